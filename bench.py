@@ -1,0 +1,225 @@
+"""Benchmark of the fenix brute-force kNN hot path on MI355X.
+
+Workload (BASELINE.json configs[1], the headline metric's config): one query,
+10M x 768 float32 rows per GPU, L2, k=100, corpus resident in HBM.  One
+"step" = one exact search = fused scan + top-k over every row of this rank's
+shard, merge to the final sorted k, and for N > 1 the RCCL all-gather of the
+per-rank top-k plus the final merge (weak scaling: 10M rows per GPU, so N=8 is
+configs[3], 80M rows).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n ROWS] [--d D]
+                    [--k K] [--nq Q] [--metric l2|cosine|inner_product]
+                    [--dtype f32|f16] [--no-cpu-baseline]
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
+"""
+
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md chip table
+
+METRIC = "vectors/sec + %HBM roofline, 10M×768 f32 L2 kNN k=100 at 1/2/4/8 GPU"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--n", type=int, default=10_000_000, help="rows per GPU")
+    p.add_argument("--d", type=int, default=768)
+    p.add_argument("--k", type=int, default=100)
+    p.add_argument("--nq", type=int, default=1)
+    p.add_argument("--metric", default="l2")
+    p.add_argument("--dtype", default="f32", choices=["f32", "f16"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-rows", type=int, default=1_000_000)
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    return p.parse_args()
+
+
+def cpu_baseline(args):
+    """Oracle C restatement (float32 direct formulas, OpenMP, heap top-k) on a
+    bounded sample of the same workload, timed on this host's cores."""
+    from oracle import oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = min(threads, len(os.sched_getaffinity(0)))
+    rows = min(args.cpu_rows, args.n)
+    x = np.empty((rows, args.d), dtype=np.float32)
+    O.lib().fx_ref_fill(O._ptr(x), rows, args.d, 0, 0, 0)
+    if args.dtype == "f16":
+        x = x.astype(np.float16)
+    q = O.fill_normal(1, args.d, 1)
+    O.knn(x[: min(rows, 10000)], q, args.metric, args.k, precision=32, threads=threads)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        O.knn(x, q, args.metric, args.k, precision=32, threads=threads)
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    return {
+        "value": rows * done / el,
+        "unit": "vectors/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{rows}x{args.d} {args.dtype} {args.metric} k={args.k}, {done} single-query "
+        f"searches in {el:.1f}s (oracle/knn_ref.c precision=32, same generator)",
+    }
+
+
+def pmc_traffic(workload_tag):
+    """HBM bytes per scan launch from the committed rocprofv3 --pmc summary
+    (profiles/*pmc*.json, FETCH_SIZE x2 gfx950 correction already applied)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if rec.get("workload") == workload_tag and "hbm_bytes_per_launch" in rec:
+            return float(rec["hbm_bytes_per_launch"])
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from fenix_amd import _lib
+    from fenix_amd.distributed import allgather_topk
+    from fenix_amd.engine import Engine, Shard
+
+    eng = Engine.get(device)
+    tdt = torch.float32 if args.dtype == "f32" else torch.float16
+    esize = 4 if args.dtype == "f32" else 2
+    metric = _lib.METRICS[args.metric]
+    n, d, k, nq = args.n, args.d, args.k, args.nq
+    row_base = rank * n
+    x = torch.empty((n, d), dtype=tdt, device=device)
+    eng.fill(x, seed=0, row_base=row_base)
+    qh = torch.empty((nq, d), dtype=tdt, device=device)
+    eng.fill(qh, seed=1)
+    q = qh.to(torch.float32)
+    shard = Shard(x, row_base)
+    od = torch.empty((nq, k), dtype=torch.float32, device=device)
+    orow = torch.empty((nq, k), dtype=torch.int64, device=device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record()
+        ws = eng.scan(shard, q, metric, k)
+        if i is not None:
+            ev[i][1].record()
+        eng.reduce(shard, nq, metric, k, ws, od, orow)
+        if world > 1:
+            gd, gr = allgather_topk(od, orow)
+            return eng.merge(gd, gr, k)
+        return od, orow
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        res = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    scan_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, scan_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, scan_ms = float(t[0]), float(t[1])
+
+    # sanity: the last result is sorted and complete
+    rd, rr = res[0].cpu().numpy(), res[1].cpu().numpy()
+    assert (rr >= 0).all() and np.all(np.diff(rd, axis=1) >= 0), "bench result not sorted"
+
+    total_rows = n * world
+    value = total_rows * nq * args.steps / elapsed
+    scan_bytes = n * d * esize + nq * d * 4
+    achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
+    tag = f"{n}x{d}_{args.dtype}_{args.metric}_k{k}_q{nq}"
+    traffic = pmc_traffic(tag)
+
+    out = None
+    if rank == 0:
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
+        wl = (f"{n // 1_000_000 if n % 1_000_000 == 0 else n}"
+              f"{'M' if n % 1_000_000 == 0 else ''}x{d} {args.dtype} {args.metric.upper()} "
+              f"kNN k={k}, {'single query' if nq == 1 else f'{nq}-query batch'}, per GPU")
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "vectors/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic: portable Irwin-Hall(4) N(0,1) generator on device "
+                    "(corpus seed 0, query seed 1), corpus resident in HBM",
+            "config": {
+                "workload": wl,
+                "rows_per_gpu": n,
+                "total_rows": total_rows,
+                "d": d,
+                "k": k,
+                "queries": nq,
+                "metric": args.metric,
+                "parallelism": f"row-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "fx::scan_kernel (fused distance + per-wave top-k)",
+                "kernel_ms": scan_ms,
+                "bytes_per_launch": scan_bytes,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

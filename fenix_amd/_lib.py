@@ -1,0 +1,131 @@
+"""ctypes binding of the gfx950 C ABI (``include/fenix_knn.h``).
+
+The shared library is built in-tree by ``__graft_entry__.build()``
+(``make -C fenix_amd/csrc`` -> ``fenix_amd/lib/libfenix_knn.so``).  There is no
+CPU fallback: if the library or a GPU is missing, every search raises.
+Error mapping mirrors the reference's surface: bad arguments -> ``ValueError``
+(coder.py:50 raises ``ValueError()`` for an unknown metric), unsupported
+shapes -> ``NotImplementedError``, HIP failures -> ``RuntimeError``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libfenix_knn.so")
+
+DTYPE_F32 = 0
+DTYPE_F16 = 1
+METRIC_L2 = 0
+METRIC_IP = 1
+METRIC_COS = 2
+
+# coder.py:38-50: the metric names fenix accepts and their aliases
+METRICS = {
+    "l2": METRIC_L2,
+    "euclidean": METRIC_L2,
+    "inner_product": METRIC_IP,
+    "dot": METRIC_IP,
+    "cosine": METRIC_COS,
+}
+
+# every symbol include/fenix_knn.h declares
+SYMBOLS = (
+    "fx_version",
+    "fx_last_error",
+    "fx_device_count",
+    "fx_max_k",
+    "fx_knn_workspace_bytes",
+    "fx_knn_search",
+    "fx_knn_scan",
+    "fx_knn_reduce",
+    "fx_knn_distances",
+    "fx_topk_merge_workspace_bytes",
+    "fx_topk_merge",
+    "fx_fill_normal",
+)
+
+_lock = threading.Lock()
+_lib = None
+
+
+class FenixHipError(RuntimeError):
+    """A HIP runtime failure inside the kNN engine."""
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and type the shared library; raise loudly if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"fenix_amd HIP library not built: {LIB_PATH} is missing "
+                "(run __graft_entry__.build() or `make -C fenix_amd/csrc`)"
+            )
+        L = ctypes.CDLL(LIB_PATH)
+        i64, sz, vp, ci = ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
+        L.fx_version.argtypes = []
+        L.fx_version.restype = ci
+        L.fx_last_error.argtypes = []
+        L.fx_last_error.restype = ctypes.c_char_p
+        L.fx_device_count.argtypes = [ctypes.POINTER(ci)]
+        L.fx_device_count.restype = ci
+        L.fx_max_k.argtypes = []
+        L.fx_max_k.restype = i64
+        L.fx_knn_workspace_bytes.argtypes = [i64, i64, ci, i64, i64, ctypes.POINTER(sz)]
+        L.fx_knn_workspace_bytes.restype = ci
+        L.fx_knn_search.argtypes = [vp, ci, i64, i64, i64, vp, i64, ci, i64, vp, vp, sz, vp, vp,
+                                    vp]
+        L.fx_knn_search.restype = ci
+        L.fx_knn_scan.argtypes = [vp, ci, i64, i64, i64, vp, i64, ci, i64, vp, vp, sz, vp]
+        L.fx_knn_scan.restype = ci
+        L.fx_knn_reduce.argtypes = [vp, ci, i64, i64, i64, ci, i64, vp, sz, vp, vp, vp]
+        L.fx_knn_reduce.restype = ci
+        L.fx_knn_distances.argtypes = [vp, ci, i64, i64, vp, i64, ci, vp, vp, vp]
+        L.fx_knn_distances.restype = ci
+        L.fx_topk_merge_workspace_bytes.argtypes = [i64, i64, i64, i64, ctypes.POINTER(sz)]
+        L.fx_topk_merge_workspace_bytes.restype = ci
+        L.fx_topk_merge.argtypes = [vp, vp, i64, i64, i64, i64, vp, sz, vp, vp, vp]
+        L.fx_topk_merge.restype = ci
+        L.fx_fill_normal.argtypes = [vp, ci, i64, i64, ctypes.c_uint64, i64, i64, vp]
+        L.fx_fill_normal.restype = ci
+        _lib = L
+        return L
+
+
+def check(rc: int) -> None:
+    if rc == 0:
+        return
+    msg = (load().fx_last_error() or b"").decode(errors="replace")
+    if rc == -1:
+        raise ValueError(msg)
+    if rc == -2:
+        raise NotImplementedError(msg)
+    raise FenixHipError(msg)
+
+
+def max_k() -> int:
+    return int(load().fx_max_k())
+
+
+def knn_workspace_bytes(n: int, d: int, dtype: int, nq: int, k: int) -> int:
+    out = ctypes.c_size_t(0)
+    check(load().fx_knn_workspace_bytes(n, d, dtype, nq, k, ctypes.byref(out)))
+    return int(out.value)
+
+
+def merge_workspace_bytes(nq: int, parts: int, kin: int, k: int) -> int:
+    out = ctypes.c_size_t(0)
+    check(load().fx_topk_merge_workspace_bytes(nq, parts, kin, k, ctypes.byref(out)))
+    return int(out.value)
+
+
+def device_count() -> int:
+    c = ctypes.c_int(0)
+    check(load().fx_device_count(ctypes.byref(c)))
+    return int(c.value)

@@ -1,0 +1,344 @@
+// extern "C" entry points declared in include/fenix_knn.h, plus the error and
+// device-property helpers the kernels' planners use.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "fx_internal.h"
+
+namespace fx {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  return FX_OK;
+}
+
+static std::mutex g_mu;
+
+int device_cus(int* out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) {
+    set_error("hipGetDevice: %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  static std::map<int, int> cache;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) {
+    *out = it->second;
+    return FX_OK;
+  }
+  int cus = 0;
+  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) {
+    set_error("hipDeviceGetAttribute: %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  cache[dev] = cus;
+  *out = cus;
+  return FX_OK;
+}
+
+int kernel_occupancy(const void* fn, int block, size_t smem, int* out) {
+  static std::map<std::pair<const void*, size_t>, int> cache;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto key = std::make_pair(fn, smem);
+  auto it = cache.find(key);
+  if (it != cache.end()) {
+    *out = it->second;
+    return FX_OK;
+  }
+  if (smem > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  int nb = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, block, smem);
+  if (e != hipSuccess) {
+    set_error("hipOccupancyMaxActiveBlocksPerMultiprocessor: %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  cache[key] = nb;
+  *out = nb;
+  return FX_OK;
+}
+
+static size_t align256(size_t v) { return (v + 255) / 256 * 256; }
+
+static int validate(int64_t n, int64_t d, int dtype, int64_t nq, int metric) {
+  if (n < 1 || d < 1 || nq < 1) {
+    set_error("invalid shape n=%lld d=%lld nq=%lld", (long long)n, (long long)d, (long long)nq);
+    return FX_EINVAL;
+  }
+  if (d > (1 << 20)) {
+    set_error("d=%lld too large", (long long)d);
+    return FX_EUNSUPPORTED;
+  }
+  if (dtype != FX_DTYPE_F32 && dtype != FX_DTYPE_F16) {
+    set_error("unsupported dtype %d", dtype);
+    return FX_EINVAL;
+  }
+  if (metric < FX_METRIC_L2 || metric > FX_METRIC_COS) {
+    set_error("unsupported metric %d", metric);
+    return FX_EINVAL;
+  }
+  return FX_OK;
+}
+
+static constexpr int64_t kMaxK = 1024;
+
+struct SearchLayout {
+  ScanPlan scan;
+  MergePlan merge;
+  size_t lists_bytes, total;
+};
+
+static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
+                       bool aligned, SearchLayout* s) {
+  int rc = plan_scan(n, d, dtype, k, metric, aligned, &s->scan);
+  if (rc) return rc;
+  rc = plan_merge(nq, s->scan.nlists, k, k, &s->merge);
+  if (rc) return rc;
+  s->lists_bytes = align256((size_t)nq * s->scan.nlists * k * 8);
+  s->total = s->lists_bytes + s->merge.ws_bytes;
+  return FX_OK;
+}
+
+}  // namespace fx
+
+using namespace fx;
+
+extern "C" {
+
+int fx_version(void) { return 100; }
+
+const char* fx_last_error(void) { return g_err; }
+
+int fx_device_count(int* out) {
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    set_error("hipGetDeviceCount: %s", hipGetErrorString(e));
+    *out = 0;
+    return FX_EHIP;
+  }
+  *out = c;
+  return FX_OK;
+}
+
+int64_t fx_max_k(void) { return kMaxK; }
+
+int fx_knn_workspace_bytes(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k,
+                           size_t* out_bytes) {
+  if (!out_bytes) {
+    set_error("out_bytes is null");
+    return FX_EINVAL;
+  }
+  int rc = validate(n, d, dtype, nq, 0);
+  if (rc) return rc;
+  if (k < 1 || k > kMaxK) {
+    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kMaxK);
+    return FX_EUNSUPPORTED;
+  }
+  size_t best = 0;
+  for (int metric = 0; metric < 3; ++metric) {
+    for (int aligned = 0; aligned < 2; ++aligned) {
+      SearchLayout s;
+      rc = plan_search(n, d, dtype, nq, k, metric, aligned != 0, &s);
+      if (rc) return rc;
+      if (s.total > best) best = s.total;
+    }
+  }
+  *out_bytes = best;
+  return FX_OK;
+}
+
+static int search_layout(const void* corpus, int dtype, int64_t n, int64_t d, int64_t nq,
+                         int metric, int64_t k, void* ws, size_t ws_bytes, SearchLayout* s) {
+  int rc = validate(n, d, dtype, nq, metric);
+  if (rc) return rc;
+  if (k < 1 || k > kMaxK) {
+    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kMaxK);
+    return FX_EUNSUPPORTED;
+  }
+  if (!corpus || !ws) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  const bool aligned = ((uintptr_t)corpus % 16) == 0;
+  rc = plan_search(n, d, dtype, nq, k, metric, aligned, s);
+  if (rc) return rc;
+  if (ws_bytes < s->total) {
+    set_error("workspace too small: %zu < %zu", ws_bytes, s->total);
+    return FX_EINVAL;
+  }
+  return FX_OK;
+}
+
+int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                const float* queries, int64_t nq, int metric, int64_t k,
+                const uint32_t* mask, void* ws, size_t ws_bytes, void* stream) {
+  SearchLayout s;
+  int rc = search_layout(corpus, dtype, n, d, nq, metric, k, ws, ws_bytes, &s);
+  if (rc) return rc;
+  if (!queries) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  if (row_base < 0 || row_base + n >= 0xffffffffll) {
+    set_error("global rows [%lld, %lld) exceed the 32-bit row space", (long long)row_base,
+              (long long)(row_base + n));
+    return FX_EUNSUPPORTED;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  uint64_t* lists = reinterpret_cast<uint64_t*>(ws);
+  ScanArgs a = {};
+  a.X = corpus;
+  a.n = n;
+  a.d = (int)d;
+  a.row_base = row_base;
+  a.mask = mask;
+  a.rows_per_block = s.scan.rows_per_block;
+  a.k = (int)k;
+  a.cap = s.scan.cap;
+  a.qbytes = s.scan.qbytes;
+  a.mode = kModeTopk;
+  for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
+    const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
+    a.q = queries + (size_t)q0 * d;
+    a.out_lists = lists + (size_t)q0 * s.scan.nlists * k;
+    rc = launch_scan(s.scan, a, qn, st);
+    if (rc) return rc;
+  }
+  return FX_OK;
+}
+
+int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t nq, int metric,
+                  int64_t k, void* ws, size_t ws_bytes, float* out_dist, int64_t* out_row,
+                  void* stream) {
+  SearchLayout s;
+  int rc = search_layout(corpus, dtype, n, d, nq, metric, k, ws, ws_bytes, &s);
+  if (rc) return rc;
+  if (!out_dist || !out_row) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  const uint64_t* lists = reinterpret_cast<const uint64_t*>(ws);
+  void* mws = reinterpret_cast<char*>(ws) + s.lists_bytes;
+  return run_merge(s.merge, lists, nq, k, mws, out_dist, out_row,
+                   reinterpret_cast<hipStream_t>(stream));
+}
+
+int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                  const float* queries, int64_t nq, int metric, int64_t k,
+                  const uint32_t* mask, void* ws, size_t ws_bytes, float* out_dist,
+                  int64_t* out_row, void* stream) {
+  if (!out_dist || !out_row) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  int rc = fx_knn_scan(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
+                       stream);
+  if (rc) return rc;
+  return fx_knn_reduce(corpus, dtype, n, d, nq, metric, k, ws, ws_bytes, out_dist, out_row,
+                       stream);
+}
+
+int fx_knn_distances(const void* corpus, int dtype, int64_t n, int64_t d,
+                     const float* queries, int64_t nq, int metric, const uint32_t* mask,
+                     float* out, void* stream) {
+  int rc = validate(n, d, dtype, nq, metric);
+  if (rc) return rc;
+  if (!corpus || !queries || !out) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  const bool aligned = ((uintptr_t)corpus % 16) == 0;
+  ScanPlan p;
+  rc = plan_scan(n, d, dtype, 1, metric, aligned, &p);
+  if (rc) return rc;
+  ScanArgs a = {};
+  a.X = corpus;
+  a.n = n;
+  a.d = (int)d;
+  a.row_base = 0;
+  a.mask = mask;
+  a.rows_per_block = p.rows_per_block;
+  a.k = 1;
+  a.cap = p.cap;
+  a.qbytes = p.qbytes;
+  a.mode = kModeDist;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
+    const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
+    a.q = queries + (size_t)q0 * d;
+    a.out_dist = out + (size_t)q0 * n;
+    rc = launch_scan(p, a, qn, st);
+    if (rc) return rc;
+  }
+  return FX_OK;
+}
+
+int fx_topk_merge_workspace_bytes(int64_t nq, int64_t parts, int64_t kin, int64_t k,
+                                  size_t* out_bytes) {
+  if (!out_bytes || nq < 1 || parts < 1 || kin < 1 || k < 1 || k > kMaxK) {
+    set_error("invalid merge shape");
+    return FX_EINVAL;
+  }
+  MergePlan mp;
+  int rc = plan_merge(nq, parts, kin, k, &mp);
+  if (rc) return rc;
+  *out_bytes = align256((size_t)nq * parts * kin * 8) + mp.ws_bytes;
+  return FX_OK;
+}
+
+int fx_topk_merge(const float* in_dist, const int64_t* in_row, int64_t nq, int64_t parts,
+                  int64_t kin, int64_t k, void* ws, size_t ws_bytes, float* out_dist,
+                  int64_t* out_row, void* stream) {
+  size_t need = 0;
+  int rc = fx_topk_merge_workspace_bytes(nq, parts, kin, k, &need);
+  if (rc) return rc;
+  if (!in_dist || !in_row || !ws || !out_dist || !out_row) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  if (ws_bytes < need) {
+    set_error("workspace too small: %zu < %zu", ws_bytes, need);
+    return FX_EINVAL;
+  }
+  MergePlan mp;
+  rc = plan_merge(nq, parts, kin, k, &mp);
+  if (rc) return rc;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  uint64_t* comp = reinterpret_cast<uint64_t*>(ws);
+  void* mws = reinterpret_cast<char*>(ws) + align256((size_t)nq * parts * kin * 8);
+  rc = launch_encode(in_dist, in_row, nq * parts * kin, comp, st);
+  if (rc) return rc;
+  return run_merge(mp, comp, nq, k, mws, out_dist, out_row, st);
+}
+
+int fx_fill_normal(void* x, int dtype, int64_t n, int64_t d, uint64_t seed, int64_t row_base,
+                   int64_t cluster, void* stream) {
+  if (!x || n < 0 || d < 1 || (dtype != FX_DTYPE_F32 && dtype != FX_DTYPE_F16)) {
+    set_error("invalid fill arguments");
+    return FX_EINVAL;
+  }
+  return launch_fill(x, dtype, n, d, seed, row_base, cluster,
+                     reinterpret_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

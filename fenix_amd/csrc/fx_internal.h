@@ -1,0 +1,62 @@
+// Internal declarations shared by the kernel translation units and the C ABI.
+#pragma once
+
+#include "../../include/fenix_knn.h"
+#include "fx_common.h"
+
+namespace fx {
+
+constexpr int kModeTopk = 0;
+constexpr int kModeDist = 1;
+
+struct ScanArgs {
+  const void* X;          // [n][d] corpus shard
+  int64_t n;
+  int d;
+  int64_t row_base;       // global row of local row 0
+  const float* q;         // [nq][d]
+  const uint32_t* mask;   // bitmap or null
+  int64_t rows_per_block;
+  int k;
+  int cap;                // per-wave candidate list capacity
+  size_t qbytes;          // LDS bytes reserved for the query
+  int mode;               // kModeTopk / kModeDist
+  uint64_t* out_lists;    // topk: [nq][gridDim.x*4][k] composites
+  float* out_dist;        // dist: [nq][n]
+};
+
+typedef void (*ScanKernelFn)(ScanArgs);
+
+struct ScanPlan {
+  ScanKernelFn fn;
+  int W, L, U, cap;
+  size_t qbytes, smem;
+  int64_t blocks, rows_per_block, nlists;
+};
+
+int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool aligned, ScanPlan* p);
+int launch_scan(const ScanPlan& p, const ScanArgs& a, int64_t nq, hipStream_t stream);
+
+// Merge of candidate lists: [nq][nlists][kin] composites -> top-k.
+struct MergePlan {
+  int levels;
+  int64_t group[16];      // lists per block at each level
+  int64_t lists[17];      // list count entering each level (lists[levels] == 1)
+  int64_t klen[17];       // list length entering each level
+  size_t ws_bytes;        // ping-pong scratch for intermediate levels
+};
+int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p);
+int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, void* ws,
+              float* out_dist, int64_t* out_row, hipStream_t stream);
+int launch_encode(const float* dist, const int64_t* row, int64_t count, uint64_t* out,
+                  hipStream_t stream);
+int launch_fill(void* x, int dtype, int64_t n, int64_t d, uint64_t seed, int64_t row_base,
+                int64_t cluster, hipStream_t stream);
+
+// error / device helpers (capi.hip)
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+int check_launch(const char* what);
+int device_cus(int* out);
+int kernel_occupancy(const void* fn, int block, size_t smem, int* out);
+
+}  // namespace fx

@@ -1,0 +1,272 @@
+// Merge of per-wave / per-shard candidate lists into the final sorted top-k.
+//
+// Replaces the global select of the reference: pc.select_k_unstable over the
+// whole (multi-source concatenated) table, src/fenix/io/index/index.py:165-168
+// (sources concatenated by src/fenix/io/table/table.py:19-21,35).
+//
+// Each level: one 256-thread workgroup loads G lists (<= kMergeEntries
+// composites) into LDS, finds the k-th composite with a block-wide 8-bit
+// radix select, and keeps the k smallest.  Levels repeat until one list per
+// query remains; the last level bitonic-sorts it and decodes composites back
+// to (distance f32, row i64).  The candidate SET is deterministic at every
+// level (composites are unique), so the sorted output is bit-reproducible.
+#include "fx_internal.h"
+#include "fx_wave.h"
+
+namespace fx {
+
+constexpr int kMergeThreads = 256;
+constexpr int64_t kMergeEntries = 8192;  // 64 KB of composites per workgroup
+
+struct MergeShared {
+  uint32_t hist[256];
+  uint32_t sh[4];
+  uint32_t ctr_keep, ctr_eq;
+  unsigned long long shmax;
+};
+
+__device__ uint64_t block_select(const uint64_t* s, int m, int k, MergeShared* ms,
+                                 int* quota_eq) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint64_t prefix = 0, pmask = 0;
+  uint32_t need = (uint32_t)k;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    ms->hist[tid] = 0u;
+    __syncthreads();
+    for (int base = wid * kWave; base < m; base += kMergeThreads) {
+      const int i = base + lane;
+      const uint64_t e = i < m ? s[i] : kEmpty;
+      hist_add(ms->hist, (uint32_t)(e >> shift) & 255u, i < m && (e & pmask) == prefix);
+    }
+    __syncthreads();
+    if (wid == 0) {
+      const uint32_t h0 = ms->hist[4 * lane + 0], h1 = ms->hist[4 * lane + 1];
+      const uint32_t h2 = ms->hist[4 * lane + 2], h3 = ms->hist[4 * lane + 3];
+      const uint32_t sum = h0 + h1 + h2 + h3;
+      const uint32_t incl = wave_incl_scan(sum, lane), excl = incl - sum;
+      if (excl < need && need <= incl) {
+        uint32_t c = excl, digit, below, inbin;
+        if (c + h0 >= need) {
+          digit = 4 * lane; below = c; inbin = h0;
+        } else if (c + h0 + h1 >= need) {
+          digit = 4 * lane + 1; below = c + h0; inbin = h1;
+        } else if (c + h0 + h1 + h2 >= need) {
+          digit = 4 * lane + 2; below = c + h0 + h1; inbin = h2;
+        } else {
+          digit = 4 * lane + 3; below = c + h0 + h1 + h2; inbin = h3;
+        }
+        ms->sh[0] = digit;
+        ms->sh[1] = below;
+        ms->sh[2] = inbin;
+      }
+      if (lane == 0) {
+        ms->shmax = 0ull;
+        ms->sh[3] = 0u;
+      }
+    }
+    __syncthreads();
+    const uint32_t digit = ms->sh[0], below = ms->sh[1], inbin = ms->sh[2];
+    need -= below;
+    prefix |= (uint64_t)digit << shift;
+    pmask |= 0xffull << shift;
+    if (inbin == need) {
+      uint64_t mx = 0;
+      for (int i = tid; i < m; i += kMergeThreads) {
+        const uint64_t e = s[i];
+        if ((e & pmask) == prefix && e > mx) mx = e;
+      }
+      mx = wave_max_u64(mx);
+      if (lane == 0) atomicMax(&ms->shmax, (unsigned long long)mx);
+      __syncthreads();
+      const uint64_t T = ms->shmax;
+      int eq = 0;
+      for (int i = tid; i < m; i += kMergeThreads) eq += s[i] == T ? 1 : 0;
+      eq = wave_sum_i(eq);
+      if (lane == 0) atomicAdd(&ms->sh[3], (uint32_t)eq);
+      __syncthreads();
+      *quota_eq = (int)ms->sh[3];
+      __syncthreads();
+      return T;
+    }
+    __syncthreads();
+  }
+  *quota_eq = (int)need;
+  return prefix;
+}
+
+__global__ void __launch_bounds__(kMergeThreads)
+    merge_kernel(const uint64_t* __restrict__ in, int64_t nlists, int kin, int64_t G, int k,
+                 int P2, uint64_t* __restrict__ out_lists, float* __restrict__ out_dist,
+                 int64_t* __restrict__ out_row, int final_level) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  MergeShared* ms = reinterpret_cast<MergeShared*>(smem);
+  uint64_t* res = reinterpret_cast<uint64_t*>(smem + sizeof(MergeShared));
+  const int rcap = P2 > k ? P2 : k;
+  uint64_t* s = res + rcap;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int q = blockIdx.y;
+  const int64_t l0 = (int64_t)blockIdx.x * G;
+  const int nl = (int)((nlists - l0) < G ? (nlists - l0) : G);
+  const int m = nl * kin;
+  const uint64_t* src = in + ((size_t)q * nlists + l0) * (size_t)kin;
+  for (int i = tid; i < m; i += kMergeThreads) s[i] = src[i];
+  if (tid == 0) {
+    ms->ctr_keep = 0u;
+    ms->ctr_eq = 0u;
+  }
+  __syncthreads();
+
+  int nres;
+  if (m > k) {
+    int quota;
+    const uint64_t T = block_select(s, m, k, ms, &quota);
+    const uint64_t ltmask = (1ull << lane) - 1ull;
+    for (int base = wid * kWave; base < m; base += kMergeThreads) {
+      const int i = base + lane;
+      const bool in_range = i < m;
+      const uint64_t e = in_range ? s[i] : kEmpty;
+      const bool lt = in_range && e < T;
+      const bool eq = in_range && e == T;
+      const uint64_t beq = __ballot(eq);
+      uint32_t eqbase = 0;
+      if (beq) {
+        if (lane == 0) eqbase = atomicAdd(&ms->ctr_eq, (uint32_t)__popcll(beq));
+        eqbase = __shfl(eqbase, 0);
+      }
+      const bool keep = lt || (eq && (int)(eqbase + __popcll(beq & ltmask)) < quota);
+      const uint64_t bk = __ballot(keep);
+      if (bk) {
+        uint32_t pos = 0;
+        if (lane == 0) pos = atomicAdd(&ms->ctr_keep, (uint32_t)__popcll(bk));
+        pos = __shfl(pos, 0);
+        if (keep) res[pos + __popcll(bk & ltmask)] = e;
+      }
+    }
+    nres = k;
+  } else {
+    for (int i = tid; i < m; i += kMergeThreads) res[i] = s[i];
+    nres = m;
+  }
+  __syncthreads();
+  const int fill_to = final_level ? P2 : k;
+  for (int i = nres + tid; i < fill_to; i += kMergeThreads) res[i] = kEmpty;
+  __syncthreads();
+
+  if (!final_level) {
+    uint64_t* dst = out_lists + ((size_t)q * gridDim.x + blockIdx.x) * (size_t)k;
+    for (int i = tid; i < k; i += kMergeThreads) dst[i] = res[i];
+    return;
+  }
+
+  // bitonic sort of res[0..P2) ascending
+  for (int size = 2; size <= P2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < (P2 >> 1); i += kMergeThreads) {
+        const int lo = (i / stride) * 2 * stride + (i % stride);
+        const int hi = lo + stride;
+        const bool asc = (lo & size) == 0;
+        const uint64_t x = res[lo], y = res[hi];
+        if ((x > y) == asc) {
+          res[lo] = y;
+          res[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < k; i += kMergeThreads) {
+    const uint64_t e = res[i];
+    float dv;
+    int64_t rv;
+    if (e == kEmpty) {
+      dv = __builtin_nanf("");
+      rv = -1;
+    } else {
+      dv = key_float((uint32_t)(e >> 32));
+      rv = (int64_t)(e & 0xffffffffull);
+    }
+    out_dist[(size_t)q * k + i] = dv;
+    out_row[(size_t)q * k + i] = rv;
+  }
+}
+
+static int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p) {
+  if (kin > kMergeEntries / 2 || k > kMergeEntries / 2) {
+    set_error("merge list length %lld / k %lld exceeds %lld", (long long)kin, (long long)k,
+              (long long)(kMergeEntries / 2));
+    return FX_EUNSUPPORTED;
+  }
+  p->levels = 0;
+  int64_t lists = nlists, klen = kin;
+  size_t scratch = 0;
+  while (true) {
+    if (p->levels >= 16) {
+      set_error("merge tree too deep");
+      return FX_EUNSUPPORTED;
+    }
+    int64_t G = kMergeEntries / klen;
+    if (G < 2) G = 2;
+    if (G > lists) G = lists;
+    const int64_t next = (lists + G - 1) / G;
+    p->group[p->levels] = G;
+    p->lists[p->levels] = lists;
+    p->klen[p->levels] = klen;
+    p->levels++;
+    if (next > 1) {
+      const size_t bytes = (size_t)nq * next * k * 8;
+      if (bytes > scratch) scratch = bytes;
+    }
+    lists = next;
+    klen = k;
+    if (lists == 1) break;
+  }
+  p->lists[p->levels] = 1;
+  p->klen[p->levels] = k;
+  p->ws_bytes = 2 * ((scratch + 255) / 256 * 256);
+  return FX_OK;
+}
+
+int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, void* ws,
+              float* out_dist, int64_t* out_row, hipStream_t stream) {
+  const int P2 = next_pow2((int)k);
+  uint64_t* bufs[2] = {reinterpret_cast<uint64_t*>(ws),
+                       reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + p.ws_bytes / 2)};
+  const uint64_t* cur = in;
+  for (int lv = 0; lv < p.levels; ++lv) {
+    const int64_t G = p.group[lv], lists = p.lists[lv], klen = p.klen[lv];
+    const int64_t blocks = (lists + G - 1) / G;
+    const bool fin = lv == p.levels - 1;
+    uint64_t* dst = fin ? nullptr : bufs[lv & 1];
+    const int rcap = P2 > k ? P2 : (int)k;
+    const size_t smem = sizeof(MergeShared) + (size_t)rcap * 8 + (size_t)G * klen * 8;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)merge_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          160 * 1024);
+      attr_set = true;
+    }
+    for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
+      const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
+      dim3 grid((unsigned)blocks, (unsigned)qn);
+      const uint64_t* src = cur + (size_t)q0 * lists * klen;
+      uint64_t* dq = dst ? dst + (size_t)q0 * blocks * k : nullptr;
+      float* od = out_dist + (size_t)q0 * k;
+      int64_t* orow = out_row + (size_t)q0 * k;
+      hipLaunchKernelGGL(merge_kernel, grid, dim3(kMergeThreads), smem, stream, src, lists,
+                         (int)klen, G, (int)k, P2, dq, od, orow, fin ? 1 : 0);
+      int rc = check_launch("merge_kernel");
+      if (rc) return rc;
+    }
+    cur = dst;
+  }
+  return FX_OK;
+}
+
+}  // namespace fx

@@ -1,0 +1,184 @@
+"""``call`` — the brute-force search entry point, on the GPU.
+
+Drop-in for ``call`` of src/fenix/io/index/index.py:81-170 (the function
+``Server.do_exchange`` invokes, flight.py:74), brute-force branch
+(``coding=None``, ``probes=None``).  Same signature, argument meaning, output
+schema and error behaviour:
+
+* source: name or list of names under ``<root>/sources`` (index.py:93-97); a
+  ``pa.Table`` is also accepted (the reference leaves ``data`` unbound there,
+  index.py:93-99, an UnboundLocalError);
+* target: Array / ChunkedArray / FixedSizeListScalar / ndarray / Tensor,
+  normalised and cast to the column's value type exactly as index.py:101-111
+  (``pa.scalar(target, type=column type)``: a wrong length raises
+  ``ArrowInvalid``);
+* ``select`` default = every column, then ``__DISTANCE__`` appended
+  (index.py:128-129); ``assert metric is not None`` (index.py:131); an unknown
+  metric raises ``ValueError()`` (coder.py:50);
+* ``filter`` (pc.Expression) restricts the rows before the scan (index.py:161);
+* if ``maxval is not None and rows > maxval``: the ``maxval`` nearest rows,
+  ascending by distance (index.py:165-168, select_k_unstable), here with the
+  deterministic (distance, row) tie-break; otherwise every row in table order
+  with its distance (index.py:165 not taken);
+* the result is one chunk (``combine_chunks``, index.py:170); ``__DISTANCE__``
+  has the column's value type (the UDF's output type, index.py:153-159).
+
+What changes underneath: the corpus column is resident in HBM (engine.CACHE)
+instead of re-read and scanned per chunk by a Python UDF, top-k is fused into
+the gfx950 scan, and only the k winning rows are gathered (chunk-aware, no
+``Table.take`` over the whole chunked vector column, index.py:166).
+The coded (product-quantised) index — ``load``/``make``/``list``/``drop`` of
+index.py:19-78 and the ``coding``/``probes`` branch (index.py:95, 113-126) — is
+approximate search outside the MI355X hot path and raises
+``NotImplementedError``.
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.compute as pc
+import torch
+from torch import Tensor
+
+from .. import engine as _engine
+from . import coder, table
+
+CODE_COL: str = "__CODED_ID__"
+DIST_COL: str = "__DISTANCE__"
+LOCATION: str = "indexes"
+
+
+def _sources(root: str, source) -> Tuple[pa.Table, List[Tuple[Optional[str], pa.Table]]]:
+    if isinstance(source, pa.Table):
+        return source, [(None, source)]
+    names = [source] if isinstance(source, str) else list(source)
+    parts = [(table.path(root, n), table.load(root, n)) for n in names]
+    return table.join(*[t for _, t in parts]), parts
+
+
+def _target_values(target, type: pa.DataType) -> np.ndarray:
+    """index.py:101-111: normalise the target and cast it to the column type."""
+    if isinstance(target, pa.ChunkedArray):
+        target = target.combine_chunks()
+    if isinstance(target, pa.Array):
+        target = target.to_numpy(zero_copy_only=False)
+    if isinstance(target, Tensor):
+        target = target.numpy()
+    if isinstance(target, np.ndarray):
+        if pa.types.is_float16(type.value_type):
+            target = np.asarray(target).astype(np.float16)
+        target = pa.scalar(target, type=type)
+    if not isinstance(target, pa.FixedSizeListScalar):
+        raise TypeError(f"unsupported target type {type(target)}")
+    if target.type != type:
+        target = target.cast(type)
+    values = target.values.to_numpy(zero_copy_only=False)
+    return np.asarray(values, dtype=np.float32).reshape(1, -1)
+
+
+def _filter_mask(data: pa.Table, filter: pc.Expression) -> np.ndarray:
+    """Evaluate the row predicate of index.py:161 into a bool mask (nulls drop)."""
+    import pyarrow.dataset as ds
+
+    m = ds.dataset(data).to_table(columns={"__m__": filter}).column("__m__")
+    return m.fill_null(False).to_numpy(zero_copy_only=False).astype(bool)
+
+
+def _take_chunked(col: pa.ChunkedArray, rows: np.ndarray) -> pa.Array:
+    """Gather ``rows`` of a chunked column without concatenating it first."""
+    lens = np.fromiter((len(c) for c in col.chunks), dtype=np.int64, count=col.num_chunks)
+    starts = np.concatenate([[0], np.cumsum(lens)])
+    ci = np.searchsorted(starts, rows, side="right") - 1
+    order = np.argsort(ci, kind="stable")
+    pieces = []
+    for c in np.unique(ci):
+        sel = order[ci[order] == c]
+        pieces.append(col.chunk(int(c)).take(pa.array(rows[sel] - starts[c])))
+    if not pieces:
+        return pa.array([], type=col.type)
+    cat = pa.concat_arrays(pieces)
+    return cat.take(pa.array(np.argsort(order, kind="stable")))
+
+
+def take_rows(data: pa.Table, rows: np.ndarray) -> pa.Table:
+    rows = np.asarray(rows, dtype=np.int64)
+    cols = [_take_chunked(data.column(i), rows) for i in range(data.num_columns)]
+    return pa.Table.from_arrays(cols, schema=data.schema)
+
+
+def _shards(parts, column: str, device: torch.device):
+    shards, base = [], 0
+    for path, t in parts:
+        if path is not None:
+            entry = _engine.CACHE.get(path, t, column, device)
+            data = entry.shard_data
+        else:
+            data = _engine.stage_column(t.column(column), device)
+        shards.append(_engine.Shard(data, base))
+        base += t.num_rows
+    return shards
+
+
+def call(
+    root: str,
+    coding: str | None,
+    source: str | Sequence[str] | pa.Table,
+    column: str,
+    target: pa.Array | pa.ChunkedArray | pa.FixedSizeListScalar | np.ndarray | Tensor,
+    metric: str | None = None,
+    select: Sequence[str] | None = None,
+    filter: pc.Expression | None = None,
+    maxval: int | None = None,
+    probes: int | None = None,
+) -> pa.Table:
+    if coding is not None or probes is not None:
+        raise NotImplementedError(
+            "coded-index (product-quantised) search is outside the fenix_amd brute-force path"
+        )
+
+    data, parts = _sources(root, source)
+    type = data.schema.field(column).type
+    q = _target_values(target, type)
+
+    select = [*select] if select is not None else data.column_names
+    select = select + [DIST_COL]
+
+    assert metric is not None
+
+    m = coder.metric_id(metric)
+    _engine.value_dtype(type)
+
+    mask = _filter_mask(data, filter) if filter is not None else None
+    n_rows = int(mask.sum()) if mask is not None else data.num_rows
+
+    eng = _engine.Engine.get()
+    shards = _shards(parts, column, eng.device)
+    masks = None
+    if mask is not None:
+        masks = [_engine.device_mask(mask[s.row_base : s.row_base + s.n], eng.device)
+                 for s in shards]
+    qt = torch.from_numpy(q)
+    base_cols = [c for c in dict.fromkeys(select) if c != DIST_COL]
+
+    if maxval is not None and n_rows > maxval:
+        dist, rows = eng.search(shards, qt, m, int(maxval), masks)
+        dist = dist[0].cpu().numpy()
+        rows = rows[0].cpu().numpy()
+        keep = rows >= 0
+        dist, rows = dist[keep], rows[keep]
+        out = take_rows(data.select(base_cols), rows)
+    else:
+        dists = []
+        for i, s in enumerate(shards):
+            dm = masks[i] if masks is not None else None
+            dists.append(eng.distances(s, qt, m, dm)[0].cpu().numpy())
+        dist = np.concatenate(dists) if dists else np.zeros(0, np.float32)
+        out = data.select(base_cols)
+        if mask is not None:
+            out = out.filter(pa.array(mask))
+            dist = dist[mask]
+    out = out.append_column(DIST_COL, pa.array(dist.astype(type.value_type.to_pandas_dtype())))
+    return out.select(select).combine_chunks()

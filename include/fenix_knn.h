@@ -1,0 +1,147 @@
+/*
+ * fenix_knn.h — C ABI of the MI355X (gfx950) brute-force kNN engine behind
+ * fenix's search path.
+ *
+ * Reference path replaced (nrlugg/fenix, paths relative to /root/reference):
+ *   src/fenix/flight.py:242-288        Flight.search (client, unchanged API)
+ *   src/fenix/flight.py:62-77          Server.do_exchange → io.index.call
+ *   src/fenix/io/index/index.py:81-170 io.index.call (brute-force branch, coding=None)
+ *   src/fenix/io/index/index.py:133-162  per-chunk scalar UDF "distance:{metric}:{T}:{D}"
+ *   src/fenix/io/coder/coder.py:38-50  io.coder.distance (cdist / -u@v / cosine)
+ *   src/fenix/io/index/index.py:165-168  pc.select_k_unstable + Table.take
+ *
+ * The reference's pluggable boundary is Python-level (io.index.call and the
+ * pyarrow compute-function registry).  The host mirror in fenix_amd/ binds
+ * these entry points with ctypes.  All pointers are
+ * device pointers unless stated otherwise; all calls are asynchronous on the
+ * given hipStream_t (passed as void*), borrow their inputs, allocate nothing
+ * per call, and operate on the calling thread's current HIP device.
+ *
+ * Ordering contract (deterministic tie-break): results are the k smallest
+ * (distance, global_row) pairs, ascending by distance then by row.  -0.0 is
+ * treated as +0.0; NaN distances order after every number (Arrow
+ * select_k_unstable: NaN after numbers).  A slot with no candidate (fewer than
+ * k admissible rows) returns distance NaN and row -1.
+ *
+ * Row numbering: global_row = row_base + local_row; global rows must be
+ * < 2^32 - 1 (4.29 G rows per search).
+ *
+ * Return value of every int function: 0 on success, negative on failure; the
+ * message is available from fx_last_error() (thread-local).
+ */
+#ifndef FENIX_KNN_H
+#define FENIX_KNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* dtype of the corpus (the Arrow fixed_size_list value type) */
+#define FX_DTYPE_F32 0
+#define FX_DTYPE_F16 1
+
+/* metric; aliases are resolved by the host (coder.py:39 "euclidean"->l2,
+ * coder.py:47 "dot"->inner_product) */
+#define FX_METRIC_L2 0     /* sqrt(sum (x-q)^2)                      coder.py:39-40 */
+#define FX_METRIC_IP 1     /* -(x . q)                               coder.py:47-48 */
+#define FX_METRIC_COS 2    /* 0.5 - 0.5 (x/max|x|,1e-12).(q/max|q|)  coder.py:42-45 */
+
+/* error codes */
+#define FX_OK 0
+#define FX_EINVAL -1       /* bad argument (maps to ValueError / AssertionError) */
+#define FX_EUNSUPPORTED -2 /* valid but not supported by this build */
+#define FX_EHIP -3         /* HIP runtime failure (maps to RuntimeError) */
+
+/* ABI version (major*100 + minor). */
+int fx_version(void);
+
+/* Thread-local description of the last failure on this thread. */
+const char* fx_last_error(void);
+
+/* Number of visible HIP devices. */
+int fx_device_count(int* out);
+
+/* Largest k accepted by fx_knn_search. */
+int64_t fx_max_k(void);
+
+/*
+ * Workspace needed by fx_knn_search for this shape on the current device.
+ * Replaces nothing in the reference directly: the reference allocates an
+ * n-row distance column per call (index.py:162); this engine needs only
+ * candidate lists, O(nq * lists * k) bytes.
+ */
+int fx_knn_workspace_bytes(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k,
+                           size_t* out_bytes);
+
+/*
+ * Exact k-nearest-neighbour search of nq queries over one row-major corpus
+ * shard [n][d] of dtype.  Replaces index.py:162-168 (distance UDF over every
+ * chunk + select_k_unstable) for coding=None.
+ *   corpus   device, n*d elements of dtype, row-major (the Arrow values buffer)
+ *   row_base global row number of corpus row 0 (multi-source / multi-GPU shards)
+ *   queries  device, nq*d float32 (already cast to the column type: index.py:111)
+ *   mask     device bitmap over local rows (bit r of word r>>5), 1 = row is
+ *            admissible; NULL = all rows (replaces data.filter, index.py:161)
+ *   out_dist device [nq][k] float32, out_row device [nq][k] int64
+ */
+int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                  const float* queries, int64_t nq, int metric, int64_t k,
+                  const uint32_t* mask, void* ws, size_t ws_bytes, float* out_dist,
+                  int64_t* out_row, void* stream);
+
+/*
+ * fx_knn_search in two phases, for callers that overlap or time them apart:
+ * fx_knn_scan launches only the fused scan (candidate lists into ws);
+ * fx_knn_reduce launches the merge levels that turn them into out_dist /
+ * out_row.  Both must be given the same shape, metric, k and corpus alignment
+ * (the list count is planned from them).
+ */
+int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                const float* queries, int64_t nq, int metric, int64_t k,
+                const uint32_t* mask, void* ws, size_t ws_bytes, void* stream);
+int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t nq, int metric,
+                  int64_t k, void* ws, size_t ws_bytes, float* out_dist, int64_t* out_row,
+                  void* stream);
+
+/*
+ * All distances of nq queries to every corpus row: out[nq][n] float32.
+ * Replaces the per-chunk UDF / coder.distance (index.py:137-151, coder.py:38-50)
+ * where the reference returns the whole table (maxval None or n <= maxval,
+ * index.py:165).  Masked-out rows get NaN.
+ */
+int fx_knn_distances(const void* corpus, int dtype, int64_t n, int64_t d,
+                     const float* queries, int64_t nq, int metric, const uint32_t* mask,
+                     float* out, void* stream);
+
+/*
+ * Merge `parts` sorted top-k lists per query (e.g. one per GPU shard or per
+ * source) into one: in_dist/in_row [nq][parts][kin] (device), out [nq][k].
+ * Same ordering contract.  Replaces select_k over the concatenated table of
+ * several sources (table.py:19-21 + index.py:166) and is the final merge
+ * after the cross-GPU all-gather.
+ */
+int fx_topk_merge_workspace_bytes(int64_t nq, int64_t parts, int64_t kin, int64_t k,
+                                  size_t* out_bytes);
+int fx_topk_merge(const float* in_dist, const int64_t* in_row, int64_t nq, int64_t parts,
+                  int64_t kin, int64_t k, void* ws, size_t ws_bytes, float* out_dist,
+                  int64_t* out_row, void* stream);
+
+/*
+ * Portable synthetic corpus generator (test/bench data; bit-identical to
+ * oracle/knn_ref.c fx_ref_fill): element (r, c) = IrwinHall4(splitmix64(
+ * seed * 0x9E3779B97F4A7C15 + (row_base + r) * d + c)), approximately N(0,1).
+ * The clustered variant (tests/test_flight.py:21-22 of the reference)
+ * adds 10 * row[batch_start] to every row of each `cluster`-row batch
+ * (cluster <= 0: plain).
+ */
+int fx_fill_normal(void* x, int dtype, int64_t n, int64_t d, uint64_t seed, int64_t row_base,
+                   int64_t cluster, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FENIX_KNN_H */

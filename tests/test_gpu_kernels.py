@@ -1,0 +1,283 @@
+"""GPU parity of the HIP kernels against the CPU oracle, through the C ABI.
+
+Every call goes fenix_amd.engine -> ctypes -> libfenix_knn.so (gfx950);
+inputs come from the portable generator (device) and are regenerated
+bit-identically on the host for the oracle (oracle/knn_ref.c, float64).
+"""
+
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from fenix_amd import _lib
+from fenix_amd.engine import Engine, Shard, device_mask
+from oracle import oracle as O
+from tests.parity import check_topk, scale_of
+
+pytestmark = pytest.mark.gpu
+
+METRICS = ["l2", "inner_product", "cosine"]
+
+
+@pytest.fixture(scope="module")
+def eng():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return Engine.get(torch.device("cuda", 0))
+
+
+def gpu_fill(eng, n, d, seed, dtype=torch.float32, row_base=0, cluster=0):
+    x = torch.empty((n, d), dtype=dtype, device=eng.device)
+    eng.fill(x, seed, row_base, cluster)
+    return x
+
+
+def gpu_search(eng, x, q, metric, k, mask=None, row_base=0):
+    qt = torch.as_tensor(q, dtype=torch.float32).to(eng.device)
+    m = device_mask(mask, eng.device) if mask is not None else None
+    d, r = eng.search([Shard(x, row_base)], qt, _lib.METRICS[metric], k, [m])
+    torch.cuda.synchronize()
+    return d.cpu().numpy(), r.cpu().numpy()
+
+
+# ---------------------------------------------------------------- generator
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("cluster", [0, 1000])
+def test_fill_bit_exact(eng, dtype, cluster):
+    n, d = 3001, 96
+    x = gpu_fill(eng, n, d, seed=7, dtype=dtype, row_base=123, cluster=cluster).cpu().numpy()
+    ref = O.fill_normal(n, d, 7, row_base=123, cluster=cluster,
+                        dtype=np.float32 if dtype == torch.float32 else np.float16)
+    assert x.tobytes() == ref.tobytes()
+
+
+# ------------------------------------------------------------ golden vectors
+
+
+def _golden(golden_dir, name):
+    z = np.load(os.path.join(golden_dir, f"{name}.npz"))
+    return z, json.loads(str(z["meta"]))
+
+
+@pytest.mark.parametrize("name", ["g1_d128", "g1_d768", "g4_flight"])
+def test_golden_fenix_ids_and_distances(eng, golden_dir, name):
+    """GPU top-k == the reference's own io.index.call / Flight.search output."""
+    z, meta = _golden(golden_dir, name)
+    x = gpu_fill(eng, meta["n"], meta["d"], meta["seed"], cluster=meta["cluster"])
+    q = O.fill_normal(meta["nq"], meta["d"], meta["qseed"])
+    for metric in meta["metrics"]:
+        for k in meta["ks"]:
+            gd, gr = gpu_search(eng, x, q, metric, k)
+            fid = z[f"{metric}_k{k}_ids"]
+            fdist = z[f"{metric}_k{k}_dist"].astype(np.float64)
+            np.testing.assert_array_equal(gr, fid, err_msg=f"{name} {metric} k={k}")
+            rel = np.abs(gd - fdist) / np.abs(fdist)
+            assert rel.max() <= 1e-5, f"{name} {metric} k={k}: rel {rel.max():.3e}"
+
+
+def test_golden_ties(eng, golden_dir):
+    """Duplicated rows: fenix pins the tie SET; we also pin the order (row asc)."""
+    z, meta = _golden(golden_dir, "g2_ties")
+    base = O.fill_normal(1024, 64, 5)
+    x = torch.from_numpy(np.concatenate([base, base])).to(eng.device)
+    q = O.fill_normal(meta["nq"], 64, meta["qseed"])
+    for metric in meta["metrics"]:
+        gd, gr = gpu_search(eng, x, q, metric, 10)
+        fid = z[f"{metric}_k10_ids"]
+        for i in range(len(q)):
+            # same multiset of base rows (row r and r+1024 are the same vector)
+            assert sorted(gr[i] % 1024) == sorted(fid[i] % 1024)
+            # deterministic order: each pair appears (r, r+1024) consecutively
+            for j in range(0, 10, 2):
+                assert gr[i, j + 1] == gr[i, j] + 1024 and gd[i, j] == gd[i, j + 1]
+
+
+def test_golden_tail_full_table(eng, golden_dir):
+    """maxval >= rows: every distance in row order (index.py:165 not taken)."""
+    z, meta = _golden(golden_dir, "g3_tail")
+    n, d = meta["n"], meta["d"]
+    x = gpu_fill(eng, n, d, meta["seed"])
+    q = O.fill_normal(meta["nq"], d, meta["qseed"])
+    for metric in meta["metrics"]:
+        out = eng.distances(Shard(x, 0), torch.from_numpy(q), _lib.METRICS[metric])
+        got = out.cpu().numpy()
+        fid = z[f"{metric}_k{n}_ids"]
+        fdist = z[f"{metric}_k{n}_dist"].astype(np.float64)
+        np.testing.assert_array_equal(fid, np.tile(np.arange(n), (len(q), 1)))
+        xh = O.fill_normal(n, d, meta["seed"])
+        ref = O.distance_f64(xh, q, metric)
+        sc = scale_of(xh, q, metric)[:, None]
+        assert np.all(np.abs(got - ref) <= 1e-5 * np.maximum(np.abs(ref), sc))
+        # and agrees with what fenix itself returned (its own f32 error included)
+        assert np.all(np.abs(got - fdist) <= 1e-5 * np.maximum(np.abs(fdist), sc))
+
+
+# ------------------------------------------------------- random-shape parity
+
+
+CASES = [
+    # n, d, k, dtype
+    (1, 8, 1, torch.float32),
+    (5, 3, 10, torch.float32),
+    (100, 1, 7, torch.float32),
+    (1000, 17, 10, torch.float32),
+    (4097, 64, 100, torch.float32),
+    (4097, 100, 33, torch.float32),
+    (20000, 128, 10, torch.float32),
+    (20000, 384, 256, torch.float32),
+    (12345, 768, 100, torch.float32),
+    (5000, 1000, 64, torch.float32),
+    (3000, 1536, 100, torch.float32),
+    (2000, 3072, 10, torch.float32),
+    (20000, 768, 1000, torch.float32),
+    (4097, 128, 100, torch.float16),
+    (12345, 768, 100, torch.float16),
+    (5000, 1536, 1000, torch.float16),
+    (3001, 20, 10, torch.float16),
+]
+
+
+@pytest.mark.parametrize("n,d,k,dtype", CASES)
+@pytest.mark.parametrize("metric", METRICS)
+def test_random_parity(eng, n, d, k, dtype, metric):
+    x = gpu_fill(eng, n, d, seed=n + d, dtype=dtype)
+    q = O.fill_normal(3, d, seed=99)
+    xh = O.fill_normal(n, d, n + d, dtype=np.float32 if dtype == torch.float32 else np.float16)
+    qc = q.astype(xh.dtype).astype(np.float32)  # query cast to the column type (index.py:111)
+    gd, gr = gpu_search(eng, x, qc, metric, k)
+    od, orow = O.knn(xh, qc, metric, k)
+    check_topk(gd, gr, od, orow, xh.astype(np.float32), qc, metric)
+
+
+@pytest.mark.parametrize("metric", METRICS)
+def test_mask_and_row_base(eng, metric):
+    n, d, k = 30000, 256, 50
+    x = gpu_fill(eng, n, d, seed=3)
+    xh = O.fill_normal(n, d, 3)
+    q = O.fill_normal(2, d, seed=4)
+    mask = np.random.RandomState(0).rand(n) < 0.05
+    gd, gr = gpu_search(eng, x, q, metric, k, mask=mask, row_base=1_000_000)
+    od, orow = O.knn(xh, q, metric, k, mask=mask, row_base=1_000_000)
+    check_topk(gd, gr, od, orow, xh, q, metric)
+    assert mask[gr[gr >= 0] - 1_000_000].all()
+
+
+def test_mask_fewer_than_k(eng):
+    n, d, k = 1000, 32, 20
+    x = gpu_fill(eng, n, d, seed=5)
+    mask = np.zeros(n, dtype=bool)
+    mask[[3, 500, 999]] = True
+    gd, gr = gpu_search(eng, x, O.fill_normal(1, d, 6), "l2", k, mask=mask)
+    assert sorted(gr[0, :3]) == [3, 500, 999]
+    assert (gr[0, 3:] == -1).all() and np.isnan(gd[0, 3:]).all()
+    gd, gr = gpu_search(eng, x, O.fill_normal(1, d, 6), "l2", k, mask=np.zeros(n, bool))
+    assert (gr == -1).all()
+
+
+def test_unaligned_corpus_scalar_path(eng):
+    """A corpus pointer that is not 16-B aligned takes the scalar-load variant."""
+    n, d, k = 5000, 64, 10
+    big = gpu_fill(eng, n + 1, d, seed=8)
+    flat = big.reshape(-1)[1 : 1 + n * d].view(n, d)  # 4-byte offset
+    xh = O.fill_normal(n + 1, d, 8).reshape(-1)[1 : 1 + n * d].reshape(n, d)
+    q = O.fill_normal(2, d, 9)
+    for metric in METRICS:
+        gd, gr = gpu_search(eng, flat, q, metric, k)
+        od, orow = O.knn(xh, q, metric, k)
+        check_topk(gd, gr, od, orow, xh, q, metric)
+
+
+def test_nan_and_zero_rows(eng):
+    """NaN distances order after numbers; -0/+0 tie by row; duplicates by row."""
+    n, d = 300, 16
+    xh = O.fill_normal(n, d, 10)
+    xh[7] = np.nan
+    xh[11] = np.nan
+    xh[20] = 0.0
+    xh[21] = -0.0
+    xh[40] = xh[39]
+    x = torch.from_numpy(xh).to(eng.device)
+    q = O.fill_normal(1, d, 11)
+    for metric in METRICS:
+        gd, gr = gpu_search(eng, x, q, metric, n)
+        od, orow = O.knn(xh, q, metric, n)
+        check_topk(gd, gr, od, orow, np.nan_to_num(xh), q, metric)
+        assert list(gr[0, -2:]) == [7, 11]
+    # inner product against a zero row is -0.0 vs +0.0: must tie, broken by row
+    gd, gr = gpu_search(eng, x, np.zeros((1, d), np.float32), "inner_product", n)
+    zero_rows = gr[0][gd[0] == 0]
+    assert list(zero_rows) == sorted(zero_rows)
+
+
+def test_many_queries(eng):
+    n, d, k = 20000, 128, 10
+    x = gpu_fill(eng, n, d, seed=12)
+    xh = O.fill_normal(n, d, 12)
+    q = O.fill_normal(37, d, 13)
+    for metric in METRICS:
+        gd, gr = gpu_search(eng, x, q, metric, k)
+        od, orow = O.knn(xh, q, metric, k)
+        check_topk(gd, gr, od, orow, xh, q, metric)
+
+
+@pytest.mark.parametrize("metric", METRICS)
+def test_distances_kernel(eng, metric):
+    n, d = 7001, 200
+    x = gpu_fill(eng, n, d, seed=14)
+    xh = O.fill_normal(n, d, 14)
+    q = O.fill_normal(3, d, 15)
+    mask = np.random.RandomState(1).rand(n) < 0.5
+    got = eng.distances(Shard(x, 0), torch.from_numpy(q), _lib.METRICS[metric],
+                        device_mask(mask, eng.device)).cpu().numpy()
+    ref = O.distance_f64(xh, q, metric)
+    sc = {"l2": 10.0, "cosine": 1.0, "inner_product": 200.0}[metric]
+    ok = np.abs(got[:, mask] - ref[:, mask]) <= 1e-5 * np.maximum(np.abs(ref[:, mask]), sc)
+    assert ok.all()
+    assert np.isnan(got[:, ~mask]).all()
+
+
+def test_topk_merge(eng):
+    """fx_topk_merge == oracle top-k of the union (the multi-GPU final merge)."""
+    rs = np.random.RandomState(2)
+    nq, parts, kin, k = 4, 8, 50, 40
+    d = rs.randn(nq, parts, kin).astype(np.float32)
+    d[0, 0, :5] = d[0, 1, :5]  # cross-list exact ties -> row order
+    r = np.arange(nq * parts * kin).reshape(nq, parts, kin) % 100000
+    r[:, 3, 10:] = -1  # empty slots
+    d[:, 3, 10:] = np.nan
+    od, orow = eng.merge(torch.from_numpy(d).to(eng.device), torch.from_numpy(r).to(eng.device), k)
+    od, orow = od.cpu().numpy(), orow.cpu().numpy()
+    for i in range(nq):
+        valid = r[i] >= 0
+        dv, rv = d[i][valid], r[i][valid]
+        order = np.lexsort((rv, dv))[:k]
+        np.testing.assert_array_equal(orow[i], rv[order])
+        np.testing.assert_array_equal(od[i], dv[order])
+
+
+def test_sharded_equals_whole(eng):
+    """topk(all rows) == merge(topk(shard_0), topk(shard_1), ...) bit-exactly."""
+    n, d, k = 60000, 768, 100
+    x = gpu_fill(eng, n, d, seed=16)
+    q = torch.from_numpy(O.fill_normal(2, d, 17)).to(eng.device)
+    whole_d, whole_r = eng.search([Shard(x, 0)], q, 0, k)
+    cuts = [0, 13331, 40000, n]
+    shards = [Shard(x[a:b], a) for a, b in zip(cuts[:-1], cuts[1:])]
+    sd, sr = eng.search(shards, q, 0, k)
+    assert torch.equal(whole_r, sr) and torch.equal(whole_d, sd)
+
+
+def test_error_paths(eng):
+    x = gpu_fill(eng, 10, 8, seed=1)
+    q = torch.zeros((1, 8), device=eng.device)
+    with pytest.raises(NotImplementedError):
+        eng.search([Shard(x, 0)], q, 0, _lib.max_k() + 1)
+    with pytest.raises(ValueError):
+        eng.search([Shard(x, 0)], q, 7, 5)

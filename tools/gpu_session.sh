@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU session on the gpurun box: each step has its own time limit; a
+# timeout / abort / segfault ends the session (no further GPU step).
+# Usage: bash tools/gpu_session.sh STEP...   (steps: smoke tests bench prof pmc)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {
+  local name=$1 secs=$2
+  shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "   $name rc=$rc"
+  tail -n 5 "gpurun_out/$name.log"
+  case $rc in
+    0|1|2|5) return 0 ;;
+    *) echo "   stopping: $name ended with $rc"; exit "$rc" ;;
+  esac
+}
+for step in "$@"; do
+  case $step in
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    testsall) run pytest_gpu 1500 python -u -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    bench) run bench 600 python -u bench.py ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc -o run --output-format csv -- python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done"
