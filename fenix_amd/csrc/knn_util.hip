@@ -3,7 +3,7 @@
 // The generator is the device half of the portable generator whose host half
 // is oracle/knn_ref.c (fx_ref_fill) and oracle/oracle.py (fill_normal); the
 // two are bit-identical by construction (integer hash + one f32 multiply,
-// explicit _rn intrinsics for the clustered variant so nothing is contracted
+// an opaque barrier in the clustered variant so nothing is contracted
 // into an FMA).  The clustered variant is the distribution of the reference's
 // own test corpus, tests/test_flight.py:21-22 (x = x + 10 * x[0, :] per batch).
 #include "fx_internal.h"
@@ -22,7 +22,9 @@ __global__ void __launch_bounds__(256)
       float v = irwin_hall4(splitmix64(smix + g * (uint64_t)d + (uint64_t)c));
       if (cluster > 0) {
         const float v0 = irwin_hall4(splitmix64(smix + b0 * (uint64_t)d + (uint64_t)c));
-        v = __fadd_rn(v, __fmul_rn(10.0f, v0));
+        float t = 10.0f * v0;
+        asm volatile("" : "+v"(t));  // opaque: keeps the product rounded before the add
+        v = v + t;
       }
       x[r * d + c] = (T)v;
     }

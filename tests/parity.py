@@ -49,7 +49,7 @@ def check_topk(gd, gr, od, orow, x, q, metric, allow_near_ties=True):
         nv = int(valid_o.sum())
         g, o = gr[i, :nv], orow[i, :nv]
         assert len(np.unique(g)) == nv, f"query {i}: duplicate rows"
-        tol_d = DIST_RTOL * np.maximum(np.abs(od[i, :nv]), sc[i])
+        tol_d = DIST_RTOL * np.fmax(np.abs(od[i, :nv]), sc[i])
         both_nan = np.isnan(gd[i, :nv]) & np.isnan(od[i, :nv])
         err = np.where(both_nan, 0.0, np.abs(gd[i, :nv] - od[i, :nv]))
         assert np.all(err <= tol_d), (

@@ -1,0 +1,83 @@
+"""The C-ABI library loads and exports exactly what include/fenix_knn.h
+declares; argument validation runs without a GPU (no compute calls here)."""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import pytest
+
+from fenix_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fenix_knn.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(fx_\w+)\s*\(", text, re.M))
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == set(_lib.SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for sym in declared_symbols():
+        assert getattr(lib, sym) is not None
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    for sym in declared_symbols():
+        assert hasattr(raw, sym)
+
+
+def test_library_is_gfx950():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_version_and_limits():
+    lib = _lib.load()
+    assert lib.fx_version() == 100
+    assert _lib.max_k() == 1024
+
+
+def test_invalid_arguments_are_rejected_before_any_device_work():
+    with pytest.raises(ValueError, match="invalid shape"):
+        _lib.knn_workspace_bytes(0, 8, _lib.DTYPE_F32, 1, 10)
+    with pytest.raises(ValueError, match="dtype"):
+        _lib.knn_workspace_bytes(10, 8, 7, 1, 10)
+    with pytest.raises(NotImplementedError, match="k="):
+        _lib.knn_workspace_bytes(10, 8, _lib.DTYPE_F32, 1, 5000)
+    with pytest.raises(ValueError):
+        _lib.merge_workspace_bytes(1, 2, 10, 0)
+    lib = _lib.load()
+    rc = lib.fx_knn_search(None, 0, 10, 8, 0, None, 1, 0, 5, None, None, 0, None, None, None)
+    assert rc == -1 and b"null" in lib.fx_last_error()
+    rc = lib.fx_knn_distances(None, 0, 10, 8, None, 1, 9, None, None, None)
+    assert rc == -1 and b"metric" in lib.fx_last_error()
+    rc = lib.fx_fill_normal(None, 0, 10, 8, 0, 0, 0, None)
+    assert rc == -1
+
+
+def test_merge_workspace_needs_no_device():
+    assert _lib.merge_workspace_bytes(4, 8, 100, 100) >= 4 * 8 * 100 * 8
+
+
+def test_error_mapping():
+    with pytest.raises(ValueError):
+        _lib.check(-1)
+    with pytest.raises(NotImplementedError):
+        _lib.check(-2)
+    with pytest.raises(_lib.FenixHipError):
+        _lib.check(-3)
+    _lib.check(0)
+
+
+def test_metric_aliases_follow_coder():
+    # coder.py:39 euclidean == l2, coder.py:47 dot == inner_product
+    assert _lib.METRICS["euclidean"] == _lib.METRICS["l2"] == _lib.METRIC_L2
+    assert _lib.METRICS["dot"] == _lib.METRICS["inner_product"] == _lib.METRIC_IP
+    assert _lib.METRICS["cosine"] == _lib.METRIC_COS

@@ -1,0 +1,189 @@
+"""End-to-end drop-in tests, structured like the reference's
+tests/test_flight.py: an in-process Server on loopback, a 100 000 x 256
+float32 source written in 1 000-row batches with the reference's clustered
+distribution (x + 10 * x[0] per batch, test_flight.py:17-35), and searches for
+every metric.  Beyond the reference (which checks only row count and schema,
+test_flight.py:111-114) the row ids are checked against the CPU oracle."""
+
+from __future__ import annotations
+
+import socket
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.compute as pc
+import pytest
+import torch
+
+import fenix_amd
+from fenix_amd.io import index
+from oracle import oracle as O
+from tests.parity import check_topk
+
+pytestmark = pytest.mark.gpu
+
+VECTOR_SIZE = 256
+NUM_VECTORS = 100_000
+BATCH_SIZE = 1_000
+VECTOR = pa.list_(pa.float32(), list_size=VECTOR_SIZE)
+SCHEMA = pa.schema({"id": pa.int64(), "vector": VECTOR})
+METRICS = ["cosine", "dot", "inner_product", "l2", "euclidean"]
+
+
+def batches(x, batch=BATCH_SIZE, value=np.float32):
+    out = []
+    d = x.shape[1]
+    for s in range(0, x.shape[0], batch):
+        part = x[s : s + batch].astype(value)
+        a = pa.FixedSizeListArray.from_arrays(pa.array(part.ravel()), list_size=d)
+        i = pa.array(np.arange(s, s + len(part), dtype=np.int64))
+        out.append(pa.record_batch([i, a], names=["id", "vector"]))
+    return out
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def env(tmp_path_factory):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = str(tmp_path_factory.mktemp("fenix"))
+    port = _port()
+    server = fenix_amd.Server(root, host="127.0.0.1", port=port)
+    x = O.fill_normal(NUM_VECTORS, VECTOR_SIZE, seed=21, cluster=BATCH_SIZE)
+    source = pa.Table.from_batches(batches(x), SCHEMA)
+    flight = fenix_amd.Flight(host="127.0.0.1", port=port)
+    flight.make_table("test/table", source.to_reader())
+    yield dict(root=root, server=server, flight=flight, x=x, source=source)
+    server.shutdown()
+
+
+def test_make_table(env):
+    table = env["flight"].read_table("test/table").read_all()
+    assert env["source"] == table
+
+
+@pytest.mark.parametrize("metric", METRICS)
+def test_search_without_index(env, metric):
+    target = O.fill_normal(1, VECTOR_SIZE, seed=22)[0]
+    result = env["flight"].search(target=target, source="test/table", column="vector",
+                                  metric=metric, maxval=10)
+    assert result.num_rows == 10
+    assert result.schema == pa.schema([*SCHEMA, pa.field("__DISTANCE__", VECTOR.value_type)])
+    od, orow = O.knn(env["x"], target[None], metric, 10)
+    check_topk(result.column("__DISTANCE__").to_numpy()[None],
+               result.column("id").to_numpy()[None], od, orow, env["x"], target[None], metric)
+    # the gathered vectors are the rows' own vectors
+    vec = np.stack(result.column("vector").to_numpy(zero_copy_only=False))
+    np.testing.assert_array_equal(vec, env["x"][result.column("id").to_numpy()])
+
+
+def test_search_random_target_like_reference(env):
+    """The reference test's exact call: pc.random(256) cast to float32."""
+    target = pc.random(VECTOR_SIZE).cast(VECTOR.value_type)
+    for metric in METRICS:
+        r = env["flight"].search(target=target, source="test/table", column="vector",
+                                 metric=metric, maxval=10)
+        assert r.num_rows == 10
+        d = r.column("__DISTANCE__").to_numpy()
+        assert np.all(np.diff(d) >= 0)
+
+
+def test_search_select_and_filter(env):
+    target = O.fill_normal(1, VECTOR_SIZE, seed=23)[0]
+    expr = (pc.field("id") >= 30_000) & (pc.field("id") < 70_000)
+    r = env["flight"].search(target=target, source="test/table", column="vector", metric="l2",
+                             select=["id"], filter=expr, maxval=25)
+    assert r.schema == pa.schema([pa.field("id", pa.int64()),
+                                  pa.field("__DISTANCE__", pa.float32())])
+    mask = (np.arange(NUM_VECTORS) >= 30_000) & (np.arange(NUM_VECTORS) < 70_000)
+    od, orow = O.knn(env["x"], target[None], "l2", 25, mask=mask)
+    check_topk(r.column("__DISTANCE__").to_numpy()[None], r.column("id").to_numpy()[None], od,
+               orow, env["x"], target[None], "l2")
+
+
+def test_search_maxval_none_returns_whole_table(env):
+    target = O.fill_normal(1, VECTOR_SIZE, seed=24)[0]
+    r = env["flight"].search(target=target, source="test/table", column="vector", metric="cosine",
+                             select=["id"])
+    assert r.num_rows == NUM_VECTORS
+    np.testing.assert_array_equal(r.column("id").to_numpy(), np.arange(NUM_VECTORS))
+    ref = O.distances(env["x"], target[None], "cosine")[0]
+    assert np.all(np.abs(r.column("__DISTANCE__").to_numpy() - ref) <= 1e-5)
+
+
+def test_multi_source_global_rows(env):
+    root = env["root"]
+    y = O.fill_normal(5_000, VECTOR_SIZE, seed=25)
+    env["flight"].make_table("test/other", pa.Table.from_batches(batches(y), SCHEMA).to_reader())
+    target = O.fill_normal(1, VECTOR_SIZE, seed=26)[0]
+    r = index.call(root, None, ["test/other", "test/table"], "vector", target=target,
+                   metric="inner_product", maxval=50)
+    both = np.concatenate([y, env["x"]])
+    od, orow = O.knn(both, target[None], "inner_product", 50)
+    # the id column restarts per source; recover global positions from the vectors
+    vec = np.stack(r.column("vector").to_numpy(zero_copy_only=False))
+    od_ids = orow[0]
+    np.testing.assert_array_equal(vec, both[od_ids])
+
+
+def test_rewrite_restages(env):
+    root = env["root"]
+    z = O.fill_normal(3_000, VECTOR_SIZE, seed=27)
+    env["flight"].make_table("test/mut", pa.Table.from_batches(batches(z), SCHEMA).to_reader())
+    t = O.fill_normal(1, VECTOR_SIZE, seed=28)[0]
+    r1 = index.call(root, None, "test/mut", "vector", target=t, metric="l2", maxval=5)
+    z2 = O.fill_normal(3_000, VECTOR_SIZE, seed=29)
+    env["flight"].make_table("test/mut", pa.Table.from_batches(batches(z2), SCHEMA).to_reader())
+    r2 = index.call(root, None, "test/mut", "vector", target=t, metric="l2", maxval=5)
+    od, orow = O.knn(z2, t[None], "l2", 5)
+    np.testing.assert_array_equal(r2.column("id").to_numpy(), orow[0])
+    assert not r1.equals(r2)
+
+
+def test_float16_column(env):
+    root = env["root"]
+    h = O.fill_normal(20_000, 128, seed=30)
+    vt = pa.list_(pa.float16(), 128)
+    sch = pa.schema({"id": pa.int64(), "vector": vt})
+    env["flight"].make_table("test/half",
+                             pa.Table.from_batches(batches(h, value=np.float16), sch).to_reader())
+    t = O.fill_normal(1, 128, seed=31)[0]
+    r = index.call(root, None, "test/half", "vector", target=t, metric="inner_product",
+                   maxval=100)
+    assert r.schema.field("__DISTANCE__").type == pa.float16()
+    xh = h.astype(np.float16)
+    qh = t.astype(np.float16).astype(np.float32)[None]
+    od, orow = O.knn(xh, qh, "inner_product", 100)
+    # fp16 output distances: compare ids, and values at fp16 resolution
+    np.testing.assert_array_equal(r.column("id").to_numpy(), orow[0])
+    got = r.column("__DISTANCE__").to_numpy().astype(np.float64)
+    assert np.all(np.abs(got - od[0]) <= 2 ** -10 * np.abs(od[0]))
+
+
+def test_table_source_and_coder_distance(env):
+    src = env["source"].slice(0, 4_000)
+    t = O.fill_normal(1, VECTOR_SIZE, seed=32)[0]
+    r = index.call("", None, src, "vector", target=t, metric="dot", maxval=7)
+    od, orow = O.knn(env["x"][:4_000], t[None], "dot", 7)
+    np.testing.assert_array_equal(r.column("id").to_numpy(), orow[0])
+    u = torch.from_numpy(O.fill_normal(3, VECTOR_SIZE, seed=33))
+    v = torch.from_numpy(env["x"][:1000])
+    for metric in ("l2", "cosine", "dot"):
+        got = fenix_amd.io.coder.distance(u, v, metric).numpy()
+        ref = O.fenix_distance(u.numpy(), v.numpy(), metric)
+        scale = 1.0 if metric == "cosine" else float(np.abs(ref).max())
+        assert got.shape == (3, 1000)
+        assert np.all(np.abs(got - ref) <= 1e-5 * scale)
+
+
+def test_remove(env):
+    flight = env["flight"]
+    flight.remove()
+    import os
+
+    assert not os.path.exists(env["root"])

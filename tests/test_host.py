@@ -1,0 +1,163 @@
+"""Host-side logic of the drop-in surface, on CPU: target normalisation,
+filter -> mask, chunk-aware gather, storage format, error behaviour, and that
+the product path refuses to run without the GPU (no CPU fallback)."""
+
+from __future__ import annotations
+
+import os
+import pickle
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.compute as pc
+import pytest
+import torch
+
+import fenix_amd
+from fenix_amd import engine
+from fenix_amd.io import index, table
+from fenix_amd.io import torch as io_torch
+from oracle import oracle as O
+
+D = 16
+
+
+def make_source(root, name, n=2500, chunk=1000, seed=0, value=pa.float32()):
+    x = O.fill_normal(n, D, seed)
+    vt = pa.list_(value, list_size=D)
+    batches = []
+    for s in range(0, n, chunk):
+        part = x[s : s + chunk]
+        vals = pa.array(part.ravel().astype(np.float16 if value == pa.float16() else np.float32))
+        arr = pa.FixedSizeListArray.from_arrays(vals, list_size=D)
+        ids = pa.array(np.arange(s, s + len(part), dtype=np.int64))
+        batches.append(pa.record_batch([ids, arr], names=["id", "vector"]))
+    schema = pa.schema({"id": pa.int64(), "vector": vt})
+    return table.make(root, name, pa.RecordBatchReader.from_batches(schema, batches)), x
+
+
+def test_table_roundtrip_and_listing(tmp_path):
+    root = str(tmp_path)
+    t, x = make_source(root, "a/b")
+    assert t.num_rows == 2500 and t.column("vector").num_chunks == 3
+    assert table.load(root, "a/b") == t
+    both = table.load(root, ["a/b", "a/b"])
+    assert both.num_rows == 5000
+    assert list(table.list(root)) == ["a/b"]
+    table.drop(root, "a/b")
+    assert list(table.list(root)) == []
+
+
+def test_chunk_values_honours_offsets():
+    x = np.arange(40, dtype=np.float32)
+    arr = pa.FixedSizeListArray.from_arrays(pa.array(x), list_size=4)
+    sl = arr.slice(3, 4)
+    v = engine._chunk_values(sl, np.dtype(np.float32))
+    np.testing.assert_array_equal(v, x.reshape(10, 4)[3:7])
+    t = io_torch.from_arrow(sl)
+    np.testing.assert_array_equal(t.numpy(), x.reshape(10, 4)[3:7])
+
+
+def test_target_normalisation_matches_index_py():
+    t = pa.list_(pa.float32(), D)
+    q = np.arange(D, dtype=np.float32)
+    for target in (q, torch.from_numpy(q), pa.array(q), pa.chunked_array([pa.array(q)]),
+                   pa.scalar(q, type=t)):
+        np.testing.assert_array_equal(index._target_values(target, t)[0], q)
+    with pytest.raises(pa.ArrowInvalid):
+        index._target_values(np.zeros(D + 1, np.float32), t)
+    # fp16 column: the query takes the column's value type (index.py:111)
+    t16 = pa.list_(pa.float16(), D)
+    q16 = index._target_values(q / 3, t16)[0]
+    np.testing.assert_array_equal(q16, (q / 3).astype(np.float16).astype(np.float32))
+
+
+def test_filter_mask_equals_arrow_filter(tmp_path):
+    t, _ = make_source(str(tmp_path), "f")
+    expr = ((pc.field("id") > 2000) & (pc.field("id") < 2100)) | (pc.field("id") < 10)
+    m = index._filter_mask(t, expr)
+    np.testing.assert_array_equal(np.nonzero(m)[0], t.filter(expr).column("id").to_numpy())
+
+
+def test_take_rows_is_chunk_aware_and_ordered(tmp_path):
+    t, _ = make_source(str(tmp_path), "g", n=5500, chunk=700)
+    rows = np.array([5499, 0, 701, 700, 3333, 699, 12, 4200])
+    got = index.take_rows(t, rows)
+    assert got.equals(t.take(pa.array(rows)))
+    assert index.take_rows(t, np.zeros(0, np.int64)).num_rows == 0
+
+
+def test_bitmap_layout():
+    m = np.random.RandomState(0).rand(101) < 0.4
+    words = engine.bitmap(m)
+    assert words.dtype == np.uint32 and words.size == 4
+    for r in range(101):
+        assert ((int(words[r >> 5]) >> (r & 31)) & 1) == m[r]
+    np.testing.assert_array_equal(words, O.bitmap(m))
+
+
+def test_unknown_metric_is_value_error():
+    with pytest.raises(ValueError):
+        fenix_amd.io.coder.metric_id("manhattan")
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
+def test_search_fails_loudly_without_gpu(tmp_path):
+    root = str(tmp_path)
+    make_source(root, "s")
+    q = O.fill_normal(1, D, 1)[0]
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        index.call(root, None, "s", "vector", target=q, metric="l2", maxval=5)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        fenix_amd.io.coder.distance(torch.from_numpy(q), torch.from_numpy(O.fill_normal(5, D, 2)),
+                                    "l2")
+
+
+def test_call_argument_errors(tmp_path):
+    root = str(tmp_path)
+    make_source(root, "s")
+    q = O.fill_normal(1, D, 1)[0]
+    with pytest.raises(AssertionError):  # index.py:131
+        index.call(root, None, "s", "vector", target=q, metric=None, maxval=5)
+    with pytest.raises(ValueError):  # coder.py:50
+        index.call(root, None, "s", "vector", target=q, metric="hamming", maxval=5)
+    with pytest.raises(NotImplementedError):  # coded index is out of scope
+        index.call(root, "code", "s", "vector", target=q, metric="l2", maxval=5, probes=4)
+    with pytest.raises(pa.ArrowInvalid):  # index.py:111 length check
+        index.call(root, None, "s", "vector", target=q[:-1], metric="l2", maxval=5)
+
+
+def test_flight_client_asserts_metric():
+    f = fenix_amd.Flight(host="127.0.0.1", port=1)
+    with pytest.raises(AssertionError):  # flight.py:256
+        f.search(target=np.zeros(D, np.float32), source="s", column="vector", metric="bad")
+
+
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_flight_table_admin_without_gpu(tmp_path):
+    """make_table / read_table / drop_table / remove need no GPU (flight.py:34-60)."""
+    port = _free_port()
+    server = fenix_amd.Server(str(tmp_path / "root"), host="127.0.0.1", port=port)
+    try:
+        client = fenix_amd.Flight(host="127.0.0.1", port=port)
+        src, _ = make_source(str(tmp_path / "tmp"), "x")
+        client.make_table("t/x", src.to_reader())
+        got = client.read_table("t/x").read_all()
+        assert got == src
+        sel = client.read_table("t/x", select=["id"], filter=pc.field("id") < 5).read_all()
+        assert sel.column_names == ["id"] and sel.num_rows == 5
+        desc = pickle.dumps({"name": "t/x"})
+        assert desc  # the action body format is a pickled dict (flight.py:79-81)
+        client.drop_table("t/x")
+        assert not os.path.exists(tmp_path / "root" / "sources" / "t" / "x.arrow")
+        client.remove()
+        assert not os.path.exists(tmp_path / "root")
+    finally:
+        server.shutdown()
