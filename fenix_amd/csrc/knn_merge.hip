@@ -10,6 +10,8 @@
 // query remains; the last level bitonic-sorts it and decodes composites back
 // to (distance f32, row i64).  The candidate SET is deterministic at every
 // level (composites are unique), so the sorted output is bit-reproducible.
+#include <stdlib.h>
+
 #include "fx_internal.h"
 #include "fx_wave.h"
 
@@ -22,15 +24,20 @@ struct MergeShared {
   uint32_t hist[256];
   uint32_t sh[4];
   uint32_t ctr_keep, ctr_eq;
-  unsigned long long shmax;
+  unsigned long long shmax, all_or, all_and;
 };
 
-__device__ uint64_t block_select(const uint64_t* s, int m, int k, MergeShared* ms,
-                                 int* quota_eq) {
+// k-th smallest of s[0..m) (m > k).  start_shift: the byte holding the
+// highest bit in which the entries differ (higher bytes are common to all,
+// so their passes would put every entry in one bin).
+__device__ uint64_t block_select(const uint64_t* s, int m, int k, int start_shift,
+                                 uint64_t common, MergeShared* ms, int* quota_eq) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  uint64_t prefix = 0, pmask = 0;
+  // the bytes above start_shift are common to every entry: they seed the prefix
+  uint64_t pmask = start_shift >= 56 ? 0ull : (~0ull << (start_shift + 8));
+  uint64_t prefix = common & pmask;
   uint32_t need = (uint32_t)k;
-  for (int shift = 56; shift >= 0; shift -= 8) {
+  for (int shift = start_shift; shift >= 0; shift -= 8) {
     ms->hist[tid] = 0u;
     __syncthreads();
     for (int base = wid * kWave; base < m; base += kMergeThreads) {
@@ -110,17 +117,37 @@ __global__ void __launch_bounds__(kMergeThreads)
   const int nl = (int)((nlists - l0) < G ? (nlists - l0) : G);
   const int m = nl * kin;
   const uint64_t* src = in + ((size_t)q * nlists + l0) * (size_t)kin;
-  for (int i = tid; i < m; i += kMergeThreads) s[i] = src[i];
   if (tid == 0) {
     ms->ctr_keep = 0u;
     ms->ctr_eq = 0u;
+    ms->all_or = 0ull;
+    ms->all_and = ~0ull;
+  }
+  __syncthreads();
+  uint64_t v_or = 0, v_and = ~0ull;
+  for (int i = tid; i < m; i += kMergeThreads) {
+    const uint64_t e = src[i];
+    s[i] = e;
+    v_or |= e;
+    v_and &= e;
+  }
+#pragma unroll
+  for (int msk = 32; msk >= 1; msk >>= 1) {
+    v_or |= shfl_xor_u64(v_or, msk);
+    v_and &= shfl_xor_u64(v_and, msk);
+  }
+  if (lane == 0) {
+    atomicOr(&ms->all_or, (unsigned long long)v_or);
+    atomicAnd(&ms->all_and, (unsigned long long)v_and);
   }
   __syncthreads();
 
   int nres;
   if (m > k) {
     int quota;
-    const uint64_t T = block_select(s, m, k, ms, &quota);
+    const uint64_t diff = ms->all_or ^ ms->all_and;
+    const int start_shift = diff ? (63 - __clzll((long long)diff)) / 8 * 8 : 0;
+    const uint64_t T = block_select(s, m, k, start_shift, ms->all_and, ms, &quota);
     const uint64_t ltmask = (1ull << lane) - 1ull;
     for (int base = wid * kWave; base < m; base += kMergeThreads) {
       const int i = base + lane;
@@ -211,7 +238,15 @@ int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p)
       set_error("merge tree too deep");
       return FX_EUNSUPPORTED;
     }
-    int64_t G = kMergeEntries / klen;
+    // ~1.6 K entries per workgroup: enough workgroups to spread a level over
+    // the CUs, few enough levels (tools/microbench.py reduce[group=*]).
+    const int64_t target = 8 * klen > 1600 ? 8 * klen : 1600;
+    int64_t G = (target + klen - 1) / klen;
+    if (G * klen > kMergeEntries) G = kMergeEntries / klen;
+    if (const char* env = getenv("FX_MERGE_GROUP")) {  // tuning knob (tools/microbench.py)
+      const int64_t g = atoll(env);
+      if (g >= 2 && g * klen <= kMergeEntries) G = g;
+    }
     if (G < 2) G = 2;
     if (G > lists) G = lists;
     const int64_t next = (lists + G - 1) / G;

@@ -20,8 +20,34 @@
 // 8-bit radix select finds the k-th composite and compacts in place.  At the
 // end each wave writes its k best to global memory; knn_merge.hip reduces
 // those lists to the final sorted top-k.  No barriers in the main loop.
+#include <stdlib.h>
+
 #include "fx_internal.h"
 #include "fx_wave.h"
+
+// Rows in flight per 16-lane group (U) for each slot count L (slots of 16 B
+// per lane per row pass).  Tuning knobs for tools/microbench.py variant builds.
+#ifndef FX_U1
+#define FX_U1 8
+#endif
+#ifndef FX_U2
+#define FX_U2 2
+#endif
+#ifndef FX_U3
+#define FX_U3 2
+#endif
+#ifndef FX_U4
+#define FX_U4 1
+#endif
+#ifndef FX_U6
+#define FX_U6 1
+#endif
+#ifndef FX_U8
+#define FX_U8 1
+#endif
+#ifndef FX_U12
+#define FX_U12 1
+#endif
 
 namespace fx {
 
@@ -61,7 +87,24 @@ __device__ uint64_t wave_select(const uint64_t* buf, int cnt, int k, uint32_t* h
                                 int* quota_eq) {
   uint64_t prefix = 0, pmask = 0;
   uint32_t need = (uint32_t)k;
-  for (int shift = 56; shift >= 0; shift -= 8) {
+  // start at the highest byte in which the entries differ
+  uint64_t v_or = 0, v_and = ~0ull;
+  for (int i = lane; i < cnt; i += kWave) {
+    const uint64_t e = buf[i];
+    v_or |= e;
+    v_and &= e;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    v_or |= shfl_xor_u64(v_or, m);
+    v_and &= shfl_xor_u64(v_and, m);
+  }
+  const uint64_t diff = v_or ^ v_and;
+  const int start = diff ? (63 - __clzll((long long)diff)) / 8 * 8 : 0;
+  // the bytes above `start` are common to every entry: they seed the prefix
+  pmask = start >= 56 ? 0ull : (~0ull << (start + 8));
+  prefix = v_and & pmask;
+  for (int shift = start; shift >= 0; shift -= 8) {
     for (int i = lane; i < 256; i += kWave) hist[i] = 0u;
     wave_sync();
     for (int base = 0; base < cnt; base += kWave) {
@@ -142,30 +185,173 @@ __device__ int wave_compact(uint64_t* buf, int cnt, uint64_t T, int quota_eq, in
 //
 // T: element type (float / _Float16); W: elements per 16-B (or scalar) slot;
 // L: slots per lane per row pass (the row covers 16*L slots per pass, more
-// passes if the row is longer); U: rows per lane group in flight.
+// passes if the row is longer); U: rows per lane group per tile.
+//
+// Software pipeline: while a wave reduces tile i it already has tile i+1's
+// loads in flight (two register tiles, the loop unrolled by two so no moves),
+// so every wave keeps HBM requests outstanding continuously instead of
+// alternating load bursts with compute.
+
+template <typename T, int W, int L, int U>
+struct RowTile {
+  typename VecT<T, W>::type v[U][L];
+  int64_t row[U];
+  bool valid[U];
+};
+
+struct ScanCtx {
+  const ScanArgs* a;
+  const float* q_lds;
+  uint64_t* buf;
+  uint32_t* hist;
+  int S, lane, grp, jl, qi;
+  int64_t hi;
+  float qnorm;
+  bool topk;
+};
+
+template <typename T, int W, int L, int U>
+__device__ __forceinline__ void tile_load(RowTile<T, W, L, U>& t, int64_t it, int ch,
+                                          const ScanCtx& c) {
+  using V = typename VecT<T, W>::type;
+  const ScanArgs& a = *c.a;
+  const T* X = reinterpret_cast<const T*>(a.X);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    t.row[u] = it + u * 4 + c.grp;
+    t.valid[u] = t.row[u] < c.hi;
+    if (a.mask != nullptr && t.valid[u])
+      t.valid[u] = (a.mask[t.row[u] >> 5] >> (t.row[u] & 31)) & 1u;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const V* rp = reinterpret_cast<const V*>(X + t.row[u] * (int64_t)a.d);
+#pragma unroll
+    for (int cc = 0; cc < L; ++cc) {
+      const int s = ch * 16 * L + cc * 16 + c.jl;
+      if (t.valid[u] && s < c.S) {
+        t.v[u][cc] = load_stream(rp + s);
+      } else {
+        t.v[u][cc] = V(0);
+      }
+    }
+  }
+}
 
 template <typename T, int W, int L, int U, int METRIC>
+__device__ __forceinline__ void tile_accumulate(const RowTile<T, W, L, U>& t, int ch,
+                                                const ScanCtx& c, float (&acc)[U],
+                                                float (&acc2)[U]) {
+#pragma unroll
+  for (int cc = 0; cc < L; ++cc) {
+    const int s = ch * 16 * L + cc * 16 + c.jl;
+    float qv[W];
+#pragma unroll
+    for (int e = 0; e < W; ++e) qv[e] = c.q_lds[s * W + e];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int e = 0; e < W; ++e) {
+        const float x = elem<W>(t.v[u][cc], e);
+        if constexpr (METRIC == 0) {
+          const float d = x - qv[e];
+          acc[u] = fmaf(d, d, acc[u]);
+        } else if constexpr (METRIC == 1) {
+          acc[u] = fmaf(x, qv[e], acc[u]);
+        } else {
+          acc[u] = fmaf(x, qv[e], acc[u]);
+          acc2[u] = fmaf(x, x, acc2[u]);
+        }
+      }
+    }
+  }
+}
+
+// Distances of the tile's rows -> output (distance mode) or candidate list.
+template <typename T, int W, int L, int U, int METRIC>
+__device__ __forceinline__ void tile_finish(const RowTile<T, W, L, U>& t, float (&acc)[U],
+                                            float (&acc2)[U], const ScanCtx& c, uint64_t& thr,
+                                            int& cnt) {
+  const ScanArgs& a = *c.a;
+  float dist[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float s1 = sum16(acc[u]);
+    if constexpr (METRIC == 0) {
+      dist[u] = sqrtf(s1);
+    } else if constexpr (METRIC == 1) {
+      dist[u] = -s1;
+    } else {
+      const float s2 = sum16(acc2[u]);
+      const float nx = fmaxf(sqrtf(s2), 1e-12f);
+      dist[u] = 0.5f - 0.5f * (s1 / (nx * c.qnorm));
+    }
+  }
+  if (!c.topk) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (c.jl == 0 && t.row[u] < c.hi)
+        a.out_dist[(size_t)c.qi * a.n + t.row[u]] = t.valid[u] ? dist[u] : __builtin_nanf("");
+    }
+    return;
+  }
+  const uint64_t ltmask = (1ull << c.lane) - 1ull;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint64_t comp = make_comp(dist[u], (uint32_t)(a.row_base + t.row[u]));
+    const bool p = (c.jl == 0) && t.valid[u] && comp < thr;
+    const uint64_t b = __ballot(p);
+    if (b) {
+      if (p) c.buf[cnt + __popcll(b & ltmask)] = comp;
+      cnt += __popcll(b);
+    }
+  }
+  if (cnt > a.cap - 4 * U) {
+    wave_sync();
+    int quota;
+    thr = wave_select(c.buf, cnt, a.k, c.hist, c.lane, &quota);
+    cnt = wave_compact(c.buf, cnt, thr, quota, c.lane);
+  }
+}
+
+template <typename T, int W, int L, int U, int METRIC>
+__device__ __forceinline__ void tile_consume(const RowTile<T, W, L, U>& t, const ScanCtx& c,
+                                             uint64_t& thr, int& cnt) {
+  float acc[U], acc2[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = acc2[u] = 0.f;
+  tile_accumulate<T, W, L, U, METRIC>(t, 0, c, acc, acc2);
+  tile_finish<T, W, L, U, METRIC>(t, acc, acc2, c, thr, cnt);
+}
+
+template <typename T, int W, int L, int U, int METRIC, bool PIPE>
 __global__ void __launch_bounds__(256) scan_kernel(ScanArgs a) {
-  using V = typename VecT<T, W>::type;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int grp = lane >> 4, jl = lane & 15;
   const int S = a.d / W;
   constexpr int CH = 16 * L;
   const int nch = (S + CH - 1) / CH;
   const int qfl = nch * CH * W;  // padded query floats
 
   float* q_lds = reinterpret_cast<float*>(smem);
-  uint64_t* buf = reinterpret_cast<uint64_t*>(smem + a.qbytes) + (size_t)wid * a.cap;
-  uint32_t* hist =
-      reinterpret_cast<uint32_t*>(smem + a.qbytes + (size_t)4 * a.cap * 8) + wid * 256;
-
   const int qi = blockIdx.y;
   const float* qg = a.q + (size_t)qi * a.d;
   for (int i = threadIdx.x; i < qfl; i += 256) q_lds[i] = i < a.d ? qg[i] : 0.f;
   __syncthreads();
-  float qnorm = 1.f;
+
+  ScanCtx c;
+  c.a = &a;
+  c.q_lds = q_lds;
+  c.buf = reinterpret_cast<uint64_t*>(smem + a.qbytes) + (size_t)wid * a.cap;
+  c.hist = reinterpret_cast<uint32_t*>(smem + a.qbytes + (size_t)4 * a.cap * 8) + wid * 256;
+  c.S = S;
+  c.lane = lane;
+  c.grp = lane >> 4;
+  c.jl = lane & 15;
+  c.qi = qi;
+  c.qnorm = 1.f;
+  c.topk = a.mode == kModeTopk;
   if constexpr (METRIC == 2) {
     // F.normalize eps (coder.py:43-44): max(||q||, 1e-12); every wave reduces
     // the LDS copy itself so no extra barrier is needed.
@@ -173,153 +359,92 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanArgs a) {
     for (int i = lane; i < a.d; i += kWave) s2 = fmaf(q_lds[i], q_lds[i], s2);
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) s2 += __shfl_xor(s2, m);
-    qnorm = fmaxf(sqrtf(s2), 1e-12f);
+    c.qnorm = fmaxf(sqrtf(s2), 1e-12f);
   }
 
-  const T* X = reinterpret_cast<const T*>(a.X);
   const int64_t lo = (int64_t)blockIdx.x * a.rows_per_block;
-  const int64_t hi = lo + a.rows_per_block < a.n ? lo + a.rows_per_block : a.n;
-  const bool topk = a.mode == kModeTopk;
+  c.hi = lo + a.rows_per_block < a.n ? lo + a.rows_per_block : a.n;
+  const int64_t step = 16 * U;
 
   uint64_t thr = kEmpty;
   int cnt = 0;
+  RowTile<T, W, L, U> tA, tB;
 
-  for (int64_t it = lo + (int64_t)wid * 4 * U; it < hi; it += 16 * U) {
-    int64_t row[U];
-    bool valid[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      row[u] = it + u * 4 + grp;
-      valid[u] = row[u] < hi;
-      if (a.mask != nullptr && valid[u]) valid[u] = (a.mask[row[u] >> 5] >> (row[u] & 31)) & 1u;
+  if (PIPE && nch == 1) {
+    int64_t it = lo + (int64_t)wid * 4 * U;
+    if (it < c.hi) tile_load(tA, it, 0, c);
+    for (; it < c.hi; it += 2 * step) {
+      const int64_t it1 = it + step;
+      if (it1 < c.hi) tile_load(tB, it1, 0, c);
+      tile_consume<T, W, L, U, METRIC>(tA, c, thr, cnt);
+      if (it1 >= c.hi) break;
+      const int64_t it2 = it1 + step;
+      if (it2 < c.hi) tile_load(tA, it2, 0, c);
+      tile_consume<T, W, L, U, METRIC>(tB, c, thr, cnt);
     }
-    float acc[U], acc2[U];
+  } else {
+    // rows longer than one pass (d > 16*L*W): accumulate pass by pass
+    for (int64_t it = lo + (int64_t)wid * 4 * U; it < c.hi; it += step) {
+      float acc[U], acc2[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] = acc2[u] = 0.f;
-
-    for (int ch = 0; ch < nch; ++ch) {
-      V v[U][L];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const V* rp = reinterpret_cast<const V*>(X + row[u] * (int64_t)a.d);
-#pragma unroll
-        for (int c = 0; c < L; ++c) {
-          const int s = ch * CH + c * 16 + jl;
-          if (valid[u] && s < S) {
-            v[u][c] = load_stream(rp + s);
-          } else {
-            v[u][c] = V(0);
-          }
-        }
+      for (int u = 0; u < U; ++u) acc[u] = acc2[u] = 0.f;
+      for (int ch = 0; ch < nch; ++ch) {
+        tile_load(tA, it, ch, c);
+        tile_accumulate<T, W, L, U, METRIC>(tA, ch, c, acc, acc2);
       }
-#pragma unroll
-      for (int c = 0; c < L; ++c) {
-        const int s = ch * CH + c * 16 + jl;
-        float qv[W];
-#pragma unroll
-        for (int e = 0; e < W; ++e) qv[e] = q_lds[s * W + e];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-#pragma unroll
-          for (int e = 0; e < W; ++e) {
-            const float x = elem<W>(v[u][c], e);
-            if constexpr (METRIC == 0) {
-              const float t = x - qv[e];
-              acc[u] = fmaf(t, t, acc[u]);
-            } else if constexpr (METRIC == 1) {
-              acc[u] = fmaf(x, qv[e], acc[u]);
-            } else {
-              acc[u] = fmaf(x, qv[e], acc[u]);
-              acc2[u] = fmaf(x, x, acc2[u]);
-            }
-          }
-        }
-      }
-    }
-
-    float dist[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float s1 = sum16(acc[u]);
-      if constexpr (METRIC == 0) {
-        dist[u] = sqrtf(s1);
-      } else if constexpr (METRIC == 1) {
-        dist[u] = -s1;
-      } else {
-        const float s2 = sum16(acc2[u]);
-        const float nx = fmaxf(sqrtf(s2), 1e-12f);
-        dist[u] = 0.5f - 0.5f * (s1 / (nx * qnorm));
-      }
-    }
-
-    if (!topk) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (jl == 0 && row[u] < hi)
-          a.out_dist[(size_t)qi * a.n + row[u]] = valid[u] ? dist[u] : __builtin_nanf("");
-      }
-      continue;
-    }
-
-    const uint64_t ltmask = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t comp = make_comp(dist[u], (uint32_t)(a.row_base + row[u]));
-      const bool p = (jl == 0) && valid[u] && comp < thr;
-      const uint64_t b = __ballot(p);
-      if (b) {
-        if (p) buf[cnt + __popcll(b & ltmask)] = comp;
-        cnt += __popcll(b);
-      }
-    }
-    if (cnt > a.cap - 4 * U) {
-      wave_sync();
-      int quota;
-      thr = wave_select(buf, cnt, a.k, hist, lane, &quota);
-      cnt = wave_compact(buf, cnt, thr, quota, lane);
+      tile_finish<T, W, L, U, METRIC>(tA, acc, acc2, c, thr, cnt);
     }
   }
 
-  if (!topk) return;
+  if (!c.topk) return;
   wave_sync();
   if (cnt > a.k) {
     int quota;
-    const uint64_t kth = wave_select(buf, cnt, a.k, hist, lane, &quota);
-    cnt = wave_compact(buf, cnt, kth, quota, lane);
+    const uint64_t kth = wave_select(c.buf, cnt, a.k, c.hist, lane, &quota);
+    cnt = wave_compact(c.buf, cnt, kth, quota, lane);
   }
   uint64_t* out =
       a.out_lists + ((size_t)qi * gridDim.x * 4 + (size_t)blockIdx.x * 4 + wid) * (size_t)a.k;
-  for (int i = lane; i < a.k; i += kWave) out[i] = i < cnt ? buf[i] : kEmpty;
+  for (int i = lane; i < a.k; i += kWave) out[i] = i < cnt ? c.buf[i] : kEmpty;
 }
 
 // ----------------------------------------------------- dispatch / planning --
 
+// Double-buffered tiles everywhere except 16-bit rows of >= 12 slots, where
+// the second tile (plus the f16->f32 converts) costs more occupancy than the
+// overlap gains (tools/microbench.py sweep, profiles/r01_microbench_*.log).
+template <typename T, int L>
+constexpr bool kPipe = !(sizeof(T) == 2 && L >= 12);
+
 template <typename T, int W, int METRIC>
 static ScanKernelFn pick_l(int L) {
   switch (L) {
-    case 1: return scan_kernel<T, W, 1, 8, METRIC>;
-    case 2: return scan_kernel<T, W, 2, 4, METRIC>;
-    case 3: return scan_kernel<T, W, 3, 2, METRIC>;
-    case 4: return scan_kernel<T, W, 4, 2, METRIC>;
-    case 6: return scan_kernel<T, W, 6, 1, METRIC>;
-    case 8: return scan_kernel<T, W, 8, 1, METRIC>;
-    case 12: return scan_kernel<T, W, 12, 1, METRIC>;
-    case 16: return scan_kernel<T, W, 16, 1, METRIC>;
-    default: return scan_kernel<T, W, 24, 1, METRIC>;
+    case 1: return scan_kernel<T, W, 1, FX_U1, METRIC, kPipe<T, 1>>;
+    case 2: return scan_kernel<T, W, 2, FX_U2, METRIC, kPipe<T, 2>>;
+    case 3: return scan_kernel<T, W, 3, FX_U3, METRIC, kPipe<T, 3>>;
+    case 4: return scan_kernel<T, W, 4, FX_U4, METRIC, kPipe<T, 4>>;
+    case 6: return scan_kernel<T, W, 6, FX_U6, METRIC, kPipe<T, 6>>;
+    case 8: return scan_kernel<T, W, 8, FX_U8, METRIC, kPipe<T, 8>>;
+    case 12: return scan_kernel<T, W, 12, FX_U12, METRIC, kPipe<T, 12>>;
+    case 16: return scan_kernel<T, W, 16, 1, METRIC, kPipe<T, 16>>;
+    default: return scan_kernel<T, W, 24, 1, METRIC, kPipe<T, 24>>;
   }
 }
 
 template <typename T, int METRIC>
 static ScanKernelFn pick_scalar() {
-  return scan_kernel<T, 1, 16, 1, METRIC>;
+  return scan_kernel<T, 1, 16, 1, METRIC, true>;
 }
 
 static int rows_unroll(int L) {
   switch (L) {
-    case 1: return 8;
-    case 2: return 4;
-    case 3: return 2;
-    case 4: return 2;
+    case 1: return FX_U1;
+    case 2: return FX_U2;
+    case 3: return FX_U3;
+    case 4: return FX_U4;
+    case 6: return FX_U6;
+    case 8: return FX_U8;
+    case 12: return FX_U12;
     default: return 1;
   }
 }
@@ -389,6 +514,12 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   if (rc) return rc;
   rc = kernel_occupancy((const void*)p->fn, 256, smem, &occ);
   if (rc) return rc;
+  // Two 256-thread blocks per CU already saturate HBM with the pipelined
+  // tiles (sweep in profiles/), and fewer blocks mean fewer candidate lists
+  // to merge.  FX_SCAN_BLOCKS_PER_CU overrides (tuning knob, microbench).
+  int cap_occ = 2;
+  if (const char* env = getenv("FX_SCAN_BLOCKS_PER_CU")) cap_occ = atoi(env);
+  if (cap_occ > 0 && cap_occ < occ) occ = cap_occ;
   if (occ < 1) occ = 1;
   const int64_t max_blocks = (int64_t)cus * occ;
   // each wave should see many more rows than k for the threshold to filter

@@ -181,6 +181,23 @@ def test_mask_fewer_than_k(eng):
     assert (gr == -1).all()
 
 
+@pytest.mark.parametrize("k", [1, 10, 100, 1000])
+def test_identical_rows_select_by_row(eng, k):
+    """Every distance equal: the composites differ only in their low (row)
+    bytes, which drives both radix selects down to the last byte."""
+    n, d = 70_000, 32
+    x = torch.ones((n, d), dtype=torch.float32, device=eng.device)
+    q = np.zeros((2, d), np.float32)
+    for metric in METRICS:
+        gd, gr = gpu_search(eng, x, q, metric, k, row_base=123)
+        np.testing.assert_array_equal(gr, np.tile(np.arange(k) + 123, (2, 1)))
+        assert np.all(gd == gd[0, 0])
+    mask = np.zeros(n, dtype=bool)
+    mask[n // 2 :] = True
+    gd, gr = gpu_search(eng, x, q, "l2", k, mask=mask)
+    np.testing.assert_array_equal(gr[0], np.arange(k) + n // 2)
+
+
 def test_unaligned_corpus_scalar_path(eng):
     """A corpus pointer that is not 16-B aligned takes the scalar-load variant."""
     n, d, k = 5000, 64, 10

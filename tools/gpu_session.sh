@@ -22,10 +22,14 @@ for step in "$@"; do
   case $step in
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    testk) run pytest_kernels 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_fullsize.py -m gpu -q -x -p no:cacheprovider ;;
     testsall) run pytest_gpu 1500 python -u -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python -u bench.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc -o run --output-format csv -- python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    micro) run microbench 900 python -u tools/microbench.py --occ 0,2 --groups 0,8,16,32,64 ;;
+    sweep) run sweep 900 python -u tools/microbench.py --sweep 128:f32,256:f32,768:f32,1536:f32,768:f16,1536:f16 --occ 0,1,2,3,4 --rounds 2 --iters 6 ;;
+    vsweep) run vsweep 1100 python -u tools/microbench.py --variants --sweep 768:f32,128:f32,256:f32,768:f16,1536:f16,1536:f32,100:f32 --occ 0,2 --rounds 2 --iters 5 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
