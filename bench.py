@@ -134,7 +134,7 @@ def main():
         ws = eng.scan(shard, q, metric, k)
         if i is not None:
             ev[i][1].record()
-        eng.reduce(shard, nq, metric, k, ws, od, orow)
+        eng.reduce(shard, q, metric, k, ws, od, orow)
         if world > 1:
             gd, gr = allgather_topk(od, orow)
             return eng.merge(gd, gr, k)

@@ -84,7 +84,8 @@ def load() -> ctypes.CDLL:
         L.fx_knn_search.restype = ci
         L.fx_knn_scan.argtypes = [vp, ci, i64, i64, i64, vp, i64, ci, i64, vp, vp, sz, vp]
         L.fx_knn_scan.restype = ci
-        L.fx_knn_reduce.argtypes = [vp, ci, i64, i64, i64, ci, i64, vp, sz, vp, vp, vp]
+        L.fx_knn_reduce.argtypes = [vp, ci, i64, i64, i64, vp, i64, ci, i64, vp, vp, sz, vp, vp,
+                                    vp]
         L.fx_knn_reduce.restype = ci
         L.fx_knn_distances.argtypes = [vp, ci, i64, i64, vp, i64, ci, vp, vp, vp]
         L.fx_knn_distances.restype = ci

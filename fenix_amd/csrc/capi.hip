@@ -1,9 +1,11 @@
 // extern "C" entry points declared in include/fenix_knn.h, plus the error and
 // device-property helpers the kernels' planners use.
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 
 #include <map>
+#include <vector>
 #include <mutex>
 #include <utility>
 
@@ -101,13 +103,94 @@ static int validate(int64_t n, int64_t d, int dtype, int64_t nq, int metric) {
 
 static constexpr int64_t kMaxK = 1024;
 
+// ---------------------------------------------------------------- batched --
+//
+// Batched queries (nq >= kBatchMinQ, f32, inner product / cosine) run the
+// MFMA kernel of knn_batch.hip in phases over growing row samples:
+//   phase 0: a sample of <= cap rows, no threshold -> every (row, query) kept;
+//   phase i: a sample ~cap/(4k) times larger, threshold = the k-th composite
+//            of phase i-1 (an upper bound of the global k-th: the k-th of any
+//            row subset is), so it keeps ~cap/4 candidates per query;
+//   last:    every row with the last threshold -> final select.
+// A query whose final candidates overflow `cap` is recomputed exactly by the
+// single-query scan (fx_knn_reduce synchronises the stream once to check).
+static constexpr int64_t kBatchMinQ = 8;
+static constexpr int64_t kListLen = 4096;  // candidate buffer viewed as lists
+
+struct BatchLayout {
+  int64_t cap = 0, tiles = 0;
+  int nphases = 0;
+  int64_t start[16], stride[16], num[16];
+  MergePlan merge;
+  size_t off_qnorm, off_thr, off_count, off_cand, off_merge, total;
+};
+
+static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool aligned) {
+  if (const char* env = getenv("FX_BATCH")) {
+    if (atoi(env) == 0) return false;
+  }
+  return nq >= kBatchMinQ && dtype == FX_DTYPE_F32 &&
+         (metric == FX_METRIC_IP || metric == FX_METRIC_COS) && d % 4 == 0 && aligned;
+}
+
+static int plan_batched(int64_t n, int64_t nq, int64_t k, BatchLayout* b) {
+  const int64_t tr = batch_tile_rows();
+  b->cap = 64 * k > 16384 ? 64 * k : 16384;
+  if (const char* env = getenv("FX_BATCH_CAP")) {  // test knob: small buffers
+    const int64_t c = atoll(env);
+    if (c >= 16 * k) b->cap = c;
+  }
+  b->cap = (b->cap + kListLen - 1) / kListLen * kListLen;
+  b->tiles = (n + tr - 1) / tr;
+  // nested samples: phase i scans every stride_i-th tile, each stride a
+  // multiple of the next, so every sample contains the previous one and has
+  // at least k rows under the previous threshold; ~cap/4 appends per query.
+  const int64_t r = b->cap / (4 * k);  // >= 16 for k <= 1024
+  int64_t strides[16];
+  int m = 0;
+  strides[m++] = 1;
+  while ((b->tiles + strides[m - 1] - 1) / strides[m - 1] * tr > b->cap) {
+    if (m >= 15) {
+      set_error("batched sampling plan too deep");
+      return FX_EUNSUPPORTED;
+    }
+    strides[m] = strides[m - 1] * r;
+    ++m;
+  }
+  b->nphases = m;
+  for (int i = 0; i < m; ++i) {
+    const int64_t st = strides[m - 1 - i];
+    b->stride[i] = st;
+    b->start[i] = 0;
+    b->num[i] = (b->tiles + st - 1) / st;
+  }
+  int rc = plan_merge(nq, b->cap / kListLen, kListLen, k, &b->merge);
+  if (rc) return rc;
+  size_t off = 0;
+  b->off_qnorm = off;
+  off += align256((size_t)nq * 4);
+  b->off_thr = off;
+  off += align256((size_t)nq * 8);
+  b->off_count = off;
+  off += align256((size_t)nq * 4);
+  b->off_cand = off;
+  off += align256((size_t)nq * b->cap * 8);
+  b->off_merge = off;
+  off += align256(b->merge.ws_bytes);
+  b->total = off;
+  return FX_OK;
+}
+
 struct SearchLayout {
   ScanPlan scan;
   MergePlan merge;
   size_t lists_bytes, total;
+  bool batched;
+  BatchLayout batch;
+  size_t single_off;  // batched: workspace of the single-query fallback
 };
 
-static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
+static int plan_single(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
                        bool aligned, SearchLayout* s) {
   int rc = plan_scan(n, d, dtype, k, metric, aligned, &s->scan);
   if (rc) return rc;
@@ -115,6 +198,101 @@ static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, i
   if (rc) return rc;
   s->lists_bytes = align256((size_t)nq * s->scan.nlists * k * 8);
   s->total = s->lists_bytes + s->merge.ws_bytes;
+  s->batched = false;
+  return FX_OK;
+}
+
+static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
+                       bool aligned, SearchLayout* s) {
+  if (!use_batched(nq, dtype, metric, d, aligned)) {
+    return plan_single(n, d, dtype, nq, k, metric, aligned, s);
+  }
+  // the single-query plan (nq = 1) serves overflowing queries
+  int rc = plan_single(n, d, dtype, 1, k, metric, aligned, s);
+  if (rc) return rc;
+  const size_t single_total = s->total;
+  rc = plan_batched(n, nq, k, &s->batch);
+  if (rc) return rc;
+  s->batched = true;
+  s->single_off = s->batch.total;
+  s->total = s->batch.total + single_total;
+  return FX_OK;
+}
+
+
+// one query through the single-query scan + merge (batched-path fallback)
+static int single_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                         const float* query, int metric, int64_t k, const uint32_t* mask,
+                         void* ws, size_t ws_bytes, float* out_dist, int64_t* out_row,
+                         hipStream_t st) {
+  SearchLayout s;
+  int rc = plan_single(n, d, dtype, 1, k, metric, ((uintptr_t)corpus % 16) == 0, &s);
+  if (rc) return rc;
+  if (ws_bytes < s.total) {
+    set_error("fallback workspace too small: %zu < %zu", ws_bytes, s.total);
+    return FX_EINVAL;
+  }
+  ScanArgs a = {};
+  a.X = corpus;
+  a.n = n;
+  a.d = (int)d;
+  a.row_base = row_base;
+  a.mask = mask;
+  a.rows_per_block = s.scan.rows_per_block;
+  a.k = (int)k;
+  a.cap = s.scan.cap;
+  a.qbytes = s.scan.qbytes;
+  a.mode = kModeTopk;
+  a.q = query;
+  a.out_lists = reinterpret_cast<uint64_t*>(ws);
+  rc = launch_scan(s.scan, a, 1, st);
+  if (rc) return rc;
+  return run_merge(s.merge, a.out_lists, 1, k, reinterpret_cast<char*>(ws) + s.lists_bytes,
+                   out_dist, out_row, st);
+}
+
+static int batched_phases(const BatchLayout& b, const float* X, int64_t n, int64_t d,
+                          int64_t row_base, const float* Q, int64_t nq, int metric, int64_t k,
+                          const uint32_t* mask, char* w, hipStream_t st) {
+  float* qnorm = reinterpret_cast<float*>(w + b.off_qnorm);
+  uint64_t* thr = reinterpret_cast<uint64_t*>(w + b.off_thr);
+  uint32_t* count = reinterpret_cast<uint32_t*>(w + b.off_count);
+  uint64_t* cand = reinterpret_cast<uint64_t*>(w + b.off_cand);
+  int rc = launch_qnorm(Q, nq, (int)d, qnorm, st);
+  if (rc) return rc;
+  hipError_t e = hipMemsetAsync(thr, 0xFF, (size_t)nq * 8, st);
+  for (int ph = 0; ph < b.nphases && e == hipSuccess; ++ph) {
+    e = hipMemsetAsync(count, 0, (size_t)nq * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(cand, 0xFF, (size_t)nq * b.cap * 8, st);
+    if (e != hipSuccess) break;
+    BatchArgs a = {};
+    a.X = X;
+    a.n = n;
+    a.d = (int)d;
+    a.row_base = row_base;
+    a.Q = Q;
+    a.qnorm = qnorm;
+    a.nq = nq;
+    a.mask = mask;
+    a.tile_start = b.start[ph];
+    a.tile_stride = b.stride[ph];
+    a.num_tiles = b.num[ph];
+    a.thr = thr;
+    a.count = count;
+    a.cand = cand;
+    a.cap = (int)b.cap;
+    rc = launch_batch(a, metric, st);
+    if (rc) return rc;
+    if (ph + 1 < b.nphases) {
+      // the k-th composite of this sample bounds the global k-th from above
+      rc = run_merge(b.merge, cand, nq, k, w + b.off_merge, nullptr, nullptr, st, thr);
+      if (rc) return rc;
+    }
+  }
+  if (e != hipSuccess) {
+    set_error("batched memset: %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
   return FX_OK;
 }
 
@@ -205,6 +383,10 @@ int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row
     return FX_EUNSUPPORTED;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (s.batched) {
+    return batched_phases(s.batch, reinterpret_cast<const float*>(corpus), n, d, row_base,
+                          queries, nq, metric, k, mask, reinterpret_cast<char*>(ws), st);
+  }
   uint64_t* lists = reinterpret_cast<uint64_t*>(ws);
   ScanArgs a = {};
   a.X = corpus;
@@ -227,9 +409,10 @@ int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row
   return FX_OK;
 }
 
-int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t nq, int metric,
-                  int64_t k, void* ws, size_t ws_bytes, float* out_dist, int64_t* out_row,
-                  void* stream) {
+int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                  const float* queries, int64_t nq, int metric, int64_t k,
+                  const uint32_t* mask, void* ws, size_t ws_bytes, float* out_dist,
+                  int64_t* out_row, void* stream) {
   SearchLayout s;
   int rc = search_layout(corpus, dtype, n, d, nq, metric, k, ws, ws_bytes, &s);
   if (rc) return rc;
@@ -237,10 +420,39 @@ int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t n
     set_error("null pointer argument");
     return FX_EINVAL;
   }
-  const uint64_t* lists = reinterpret_cast<const uint64_t*>(ws);
-  void* mws = reinterpret_cast<char*>(ws) + s.lists_bytes;
-  return run_merge(s.merge, lists, nq, k, mws, out_dist, out_row,
-                   reinterpret_cast<hipStream_t>(stream));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (!s.batched) {
+    const uint64_t* lists = reinterpret_cast<const uint64_t*>(ws);
+    void* mws = reinterpret_cast<char*>(ws) + s.lists_bytes;
+    return run_merge(s.merge, lists, nq, k, mws, out_dist, out_row, st);
+  }
+  // batched: final select over the last phase's candidates
+  const BatchLayout& b = s.batch;
+  char* w = reinterpret_cast<char*>(ws);
+  const uint64_t* cand = reinterpret_cast<const uint64_t*>(w + b.off_cand);
+  rc = run_merge(b.merge, cand, nq, k, w + b.off_merge, out_dist, out_row, st);
+  if (rc) return rc;
+  // queries whose candidates overflowed `cap`: recompute exactly, one by one
+  std::vector<uint32_t> counts((size_t)nq);
+  hipError_t e = hipMemcpyAsync(counts.data(), w + b.off_count, (size_t)nq * 4,
+                                hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) {
+    set_error("batched overflow check: %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  void* sws = w + s.single_off;
+  const size_t sws_bytes = ws_bytes - s.single_off;
+  // FX_BATCH_FORCE_FALLBACK=1 (test knob) treats every query as overflowed
+  const char* force = getenv("FX_BATCH_FORCE_FALLBACK");
+  const bool all = force != nullptr && atoi(force) != 0;
+  for (int64_t q = 0; q < nq; ++q) {
+    if (!all && counts[(size_t)q] <= (uint32_t)b.cap) continue;
+    rc = single_search(corpus, dtype, n, d, row_base, queries + q * d, metric, k, mask, sws,
+                       sws_bytes, out_dist + q * k, out_row + q * k, st);
+    if (rc) return rc;
+  }
+  return FX_OK;
 }
 
 int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
@@ -254,8 +466,8 @@ int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
   int rc = fx_knn_scan(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
                        stream);
   if (rc) return rc;
-  return fx_knn_reduce(corpus, dtype, n, d, nq, metric, k, ws, ws_bytes, out_dist, out_row,
-                       stream);
+  return fx_knn_reduce(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
+                       out_dist, out_row, stream);
 }
 
 int fx_knn_distances(const void* corpus, int dtype, int64_t n, int64_t d,

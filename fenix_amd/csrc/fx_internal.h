@@ -46,8 +46,31 @@ struct MergePlan {
   size_t ws_bytes;        // ping-pong scratch for intermediate levels
 };
 int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p);
+// out_dist/out_row may be null; out_kth (optional) receives each query's k-th
+// smallest composite (kEmpty if fewer than k candidates).
 int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, void* ws,
-              float* out_dist, int64_t* out_row, hipStream_t stream);
+              float* out_dist, int64_t* out_row, hipStream_t stream,
+              uint64_t* out_kth = nullptr);
+
+// Batched queries (knn_batch.hip): fp32 MFMA GEMM + threshold filter.
+struct BatchArgs {
+  const float* X;         // [n][d] f32 corpus shard
+  int64_t n;
+  int d;
+  int64_t row_base;
+  const float* Q;         // [nq][d]
+  const float* qnorm;     // [nq] max(|q|, 1e-12) (cosine)
+  int64_t nq;
+  const uint32_t* mask;
+  int64_t tile_start, tile_stride, num_tiles;  // which 128-row tiles to scan
+  const uint64_t* thr;    // [nq] append rows whose composite <= thr
+  uint32_t* count;        // [nq] appends (may exceed cap: overflow)
+  uint64_t* cand;         // [nq][cap]
+  int cap;
+};
+int launch_batch(const BatchArgs& a, int metric, hipStream_t stream);
+int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stream);
+int batch_tile_rows();
 int launch_encode(const float* dist, const int64_t* row, int64_t count, uint64_t* out,
                   hipStream_t stream);
 int launch_fill(void* x, int dtype, int64_t n, int64_t d, uint64_t seed, int64_t row_base,

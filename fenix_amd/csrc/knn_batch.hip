@@ -1,0 +1,246 @@
+// Batched-query search: fp32 MFMA GEMM with a fused threshold filter.
+//
+// The configs[2] workload (10M x 768 f32 cosine, 256 queries) is a true dense
+// GEMM, S = X . Q^T, at 128 flop/byte — compute-bound on the matrix cores
+// (SURVEY §8(d)).  The reference evaluates it as 256 separate searches of the
+// per-chunk UDF (src/fenix/io/index/index.py:137-162 ->
+// src/fenix/io/coder/coder.py:42-48); here one pass over the corpus serves
+// every query.
+//
+// MFMA: v_mfma_f32_32x32x2_f32 (f32 in, f32 accumulate; bit-for-bit a K-ordered
+// fmaf chain, cdna_hip_programming.md §3), so batched distances carry f32
+// precision like the single-query scan.  Block = 4 waves (one per SIMD) =
+// 128 rows x 256 queries; per 32-deep K chunk the block stages X[128][32] and
+// Q[256][32] in LDS (rows padded to 36 floats: conflict-free ds_read_b128) and
+// each wave issues 8 query tiles x 16 MFMAs.  The K order inside a chunk is
+// permuted identically for A and B (lane half h reads k = 8g+4h..+3 with one
+// ds_read_b128 and feeds element t to MFMA t).  Global->LDS staging for chunk
+// c+1 is issued before chunk c's MFMAs (register prefetch, double-buffered LDS).
+//
+// Top-k without per-query lists in LDS (256 queries x k do not fit): the kernel
+// appends every (row, query) whose composite is <= the query's threshold to a
+// per-query candidate buffer in HBM (one atomic per append).  Thresholds come
+// from earlier launches of the same kernel over row samples: the k-th
+// composite of ANY subset of rows upper-bounds the global k-th, so filtering
+// with it never drops a true top-k row (capi.hip: batched_search).  The
+// buffers are then reduced by the ordinary merge kernels.
+#include "fx_internal.h"
+#include "fx_wave.h"
+
+namespace fx {
+
+constexpr int kBM = 128;        // rows per block tile
+constexpr int kBQ = 256;        // queries per block
+constexpr int kBK = 32;         // K chunk
+constexpr int kLds = kBK + 4;   // padded LDS row (floats)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct BatchShared {
+  float xs[2][kBM * kLds];
+  float qs[2][kBQ * kLds];
+  float rownorm[kBM];
+};
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// Stage one K chunk (columns [k0, k0+32)) of X rows [r0, r0+128) and of the
+// query tile into registers: X 4 x 16 B per thread, Q 8 x 16 B per thread.
+struct Prefetch {
+  f32x4 x[4];
+  f32x4 q[8];
+};
+
+__device__ __forceinline__ void prefetch_chunk(Prefetch& p, const BatchArgs& a, int64_t r0,
+                                               int64_t q0, int k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = i * 256 + tid;  // 0..1023: row = idx/8, col4 = idx%8
+    const int row = idx >> 3, c4 = idx & 7;
+    const int64_t gr = r0 + row;
+    const int k = k0 + c4 * 4;
+    if (gr < a.n && k < a.d) {
+      p.x[i] = __builtin_nontemporal_load(
+          reinterpret_cast<const f32x4*>(a.X + gr * (int64_t)a.d + k));
+    } else {
+      p.x[i] = f32x4(0.f);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int idx = i * 256 + tid;  // 0..2047: query = idx/8, col4 = idx%8
+    const int qq = idx >> 3, c4 = idx & 7;
+    const int64_t gq = q0 + qq;
+    const int k = k0 + c4 * 4;
+    p.q[i] = (gq < a.nq && k < a.d) ? ld4(a.Q + gq * (int64_t)a.d + k) : f32x4(0.f);
+  }
+}
+
+__device__ __forceinline__ void store_chunk(const Prefetch& p, BatchShared* sh, int buf, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = i * 256 + tid;
+    *reinterpret_cast<f32x4*>(&sh->xs[buf][(idx >> 3) * kLds + (idx & 7) * 4]) = p.x[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int idx = i * 256 + tid;
+    *reinterpret_cast<f32x4*>(&sh->qs[buf][(idx >> 3) * kLds + (idx & 7) * 4]) = p.q[i];
+  }
+}
+
+template <int METRIC>
+__global__ void __launch_bounds__(256, 1) batch_kernel(BatchArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  BatchShared* sh = reinterpret_cast<BatchShared*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int64_t q0 = (int64_t)blockIdx.y * kBQ;
+  const int nchunks = (a.d + kBK - 1) / kBK;
+
+  // per-lane query state for its 8 query columns
+  uint64_t thr[8];
+  float qn[8];
+#pragma unroll
+  for (int qt = 0; qt < 8; ++qt) {
+    const int64_t gq = q0 + qt * 32 + l32;
+    thr[qt] = gq < a.nq ? a.thr[gq] : 0ull;
+    qn[qt] = gq < a.nq ? a.qnorm[gq] : 1.f;
+  }
+
+  for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x) {
+    const int64_t tile = a.tile_start + ti * a.tile_stride;
+    const int64_t r0 = tile * kBM;
+    if (r0 >= a.n) continue;
+
+    f32x16 acc[8];
+#pragma unroll
+    for (int qt = 0; qt < 8; ++qt) acc[qt] = f32x16(0.f);
+    float sumsq = 0.f;
+
+    Prefetch pf;
+    prefetch_chunk(pf, a, r0, q0, 0, tid);
+    __syncthreads();  // previous tile's epilogue is done with the LDS
+    store_chunk(pf, sh, 0, tid);
+    __syncthreads();
+
+    for (int c = 0; c < nchunks; ++c) {
+      const int buf = c & 1;
+      if (c + 1 < nchunks) prefetch_chunk(pf, a, r0, q0, (c + 1) * kBK, tid);
+      const float* xs = sh->xs[buf] + (wid * 32 + l32) * kLds + 4 * h;
+      const float* qs = sh->qs[buf] + l32 * kLds + 4 * h;
+#pragma unroll
+      for (int g = 0; g < kBK / 8; ++g) {
+        const f32x4 av = ld4(xs + 8 * g);
+        if constexpr (METRIC == 2) {
+          sumsq = fmaf(av[0], av[0], sumsq);
+          sumsq = fmaf(av[1], av[1], sumsq);
+          sumsq = fmaf(av[2], av[2], sumsq);
+          sumsq = fmaf(av[3], av[3], sumsq);
+        }
+#pragma unroll
+        for (int qt = 0; qt < 8; ++qt) {
+          const f32x4 bv = ld4(qs + qt * 32 * kLds + 8 * g);
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            acc[qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], bv[t], acc[qt], 0, 0, 0);
+        }
+      }
+      if (c + 1 < nchunks) store_chunk(pf, sh, buf ^ 1, tid);
+      __syncthreads();
+    }
+
+    // ---- epilogue: distances, threshold filter, append
+    if constexpr (METRIC == 2) {
+      sumsq += __shfl_xor(sumsq, 32);
+      if (h == 0) sh->rownorm[wid * 32 + l32] = fmaxf(sqrtf(sumsq), 1e-12f);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int lr = wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int64_t row = r0 + lr;
+      bool ok = row < a.n;
+      if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
+      float nx = 1.f;
+      if constexpr (METRIC == 2) nx = sh->rownorm[lr];
+#pragma unroll
+      for (int qt = 0; qt < 8; ++qt) {
+        const float dot = acc[qt][r];
+        float dist;
+        if constexpr (METRIC == 1) {
+          dist = -dot;
+        } else {
+          dist = 0.5f - 0.5f * (dot / (nx * qn[qt]));
+        }
+        const uint64_t comp = make_comp(dist, (uint32_t)(a.row_base + row));
+        if (ok && comp <= thr[qt]) {
+          const int64_t gq = q0 + qt * 32 + l32;
+          const uint32_t pos = atomicAdd(&a.count[gq], 1u);
+          if (pos < (uint32_t)a.cap) a.cand[gq * a.cap + pos] = comp;
+        }
+      }
+    }
+  }
+}
+
+int launch_batch(const BatchArgs& a, int metric, hipStream_t stream) {
+  if (a.num_tiles <= 0) return FX_OK;
+  const size_t smem = sizeof(BatchShared);
+  const void* fn = metric == FX_METRIC_COS ? (const void*)batch_kernel<2> : (const void*)batch_kernel<1>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)batch_kernel<2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    (void)hipFuncSetAttribute((const void*)batch_kernel<1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr = true;
+  }
+  int cus = 0;
+  int rc = device_cus(&cus);
+  if (rc) return rc;
+  const int64_t qtiles = (a.nq + kBQ - 1) / kBQ;
+  int64_t bx = cus;
+  if (bx > a.num_tiles) bx = a.num_tiles;
+  for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
+    BatchArgs b = a;
+    const int64_t yn = (qtiles - y0) < 65535 ? (qtiles - y0) : 65535;
+    b.Q = a.Q + y0 * kBQ * (int64_t)a.d;
+    b.qnorm = a.qnorm + y0 * kBQ;
+    b.thr = a.thr + y0 * kBQ;
+    b.count = a.count + y0 * kBQ;
+    b.cand = a.cand + y0 * kBQ * (int64_t)a.cap;
+    b.nq = a.nq - y0 * kBQ;
+    void* args[] = {(void*)&b};
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(256), args, smem,
+                                   stream);
+    if (e != hipSuccess) {
+      set_error("batch_kernel launch: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+  }
+  return check_launch("batch_kernel");
+}
+
+int batch_tile_rows() { return kBM; }
+
+// cosine: max(||q||, 1e-12) per query (F.normalize eps, coder.py:43-44)
+__global__ void qnorm_kernel(const float* __restrict__ Q, int64_t nq, int d, float* __restrict__ out) {
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (q >= nq) return;
+  float s = 0.f;
+  for (int i = lane; i < d; i += 64) s = fmaf(Q[q * d + i], Q[q * d + i], s);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  if (lane == 0) out[q] = fmaxf(sqrtf(s), 1e-12f);
+}
+
+int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(qnorm_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, stream, Q, nq, d,
+                     out);
+  return check_launch("qnorm_kernel");
+}
+
+}  // namespace fx

@@ -104,7 +104,8 @@ __device__ uint64_t block_select(const uint64_t* s, int m, int k, int start_shif
 __global__ void __launch_bounds__(kMergeThreads)
     merge_kernel(const uint64_t* __restrict__ in, int64_t nlists, int kin, int64_t G, int k,
                  int P2, uint64_t* __restrict__ out_lists, float* __restrict__ out_dist,
-                 int64_t* __restrict__ out_row, int final_level) {
+                 int64_t* __restrict__ out_row, uint64_t* __restrict__ out_kth,
+                 int final_level) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   MergeShared* ms = reinterpret_cast<MergeShared*>(smem);
   uint64_t* res = reinterpret_cast<uint64_t*>(smem + sizeof(MergeShared));
@@ -202,6 +203,8 @@ __global__ void __launch_bounds__(kMergeThreads)
       __syncthreads();
     }
   }
+  if (out_kth != nullptr && tid == 0) out_kth[q] = res[k - 1];
+  if (out_dist == nullptr) return;
   for (int i = tid; i < k; i += kMergeThreads) {
     const uint64_t e = res[i];
     float dv;
@@ -269,7 +272,7 @@ int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p)
 }
 
 int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, void* ws,
-              float* out_dist, int64_t* out_row, hipStream_t stream) {
+              float* out_dist, int64_t* out_row, hipStream_t stream, uint64_t* out_kth) {
   const int P2 = next_pow2((int)k);
   uint64_t* bufs[2] = {reinterpret_cast<uint64_t*>(ws),
                        reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + p.ws_bytes / 2)};
@@ -292,10 +295,11 @@ int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, voi
       dim3 grid((unsigned)blocks, (unsigned)qn);
       const uint64_t* src = cur + (size_t)q0 * lists * klen;
       uint64_t* dq = dst ? dst + (size_t)q0 * blocks * k : nullptr;
-      float* od = out_dist + (size_t)q0 * k;
-      int64_t* orow = out_row + (size_t)q0 * k;
+      float* od = out_dist ? out_dist + (size_t)q0 * k : nullptr;
+      int64_t* orow = out_row ? out_row + (size_t)q0 * k : nullptr;
+      uint64_t* okth = out_kth ? out_kth + q0 : nullptr;
       hipLaunchKernelGGL(merge_kernel, grid, dim3(kMergeThreads), smem, stream, src, lists,
-                         (int)klen, G, (int)k, P2, dq, od, orow, fin ? 1 : 0);
+                         (int)klen, G, (int)k, P2, dq, od, orow, okth, fin ? 1 : 0);
       int rc = check_launch("merge_kernel");
       if (rc) return rc;
     }

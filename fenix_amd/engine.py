@@ -242,13 +242,15 @@ class Engine:
         )
         return ws
 
-    def reduce(self, shard: Shard, nq: int, metric: int, k: int, ws: torch.Tensor,
-               out_dist: torch.Tensor, out_row: torch.Tensor) -> None:
-        """Phase 2 of search_shard (fx_knn_reduce)."""
+    def reduce(self, shard: Shard, queries: torch.Tensor, metric: int, k: int, ws: torch.Tensor,
+               out_dist: torch.Tensor, out_row: torch.Tensor,
+               mask: Optional[torch.Tensor] = None) -> None:
+        """Phase 2 of search_shard (fx_knn_reduce), same arguments as scan."""
         _lib.check(
             _lib.load().fx_knn_reduce(
-                _ptr(shard.data), shard.dtype_id, shard.n, shard.d, nq, metric, k, _ptr(ws),
-                ws.numel(), _ptr(out_dist), _ptr(out_row), self._stream(),
+                _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base,
+                _ptr(queries), queries.shape[0], metric, k, _ptr(mask), _ptr(ws), ws.numel(),
+                _ptr(out_dist), _ptr(out_row), self._stream(),
             )
         )
 

@@ -94,17 +94,21 @@ int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
 
 /*
  * fx_knn_search in two phases, for callers that overlap or time them apart:
- * fx_knn_scan launches only the fused scan (candidate lists into ws);
- * fx_knn_reduce launches the merge levels that turn them into out_dist /
- * out_row.  Both must be given the same shape, metric, k and corpus alignment
- * (the list count is planned from them).
+ * fx_knn_scan launches the scan kernels (candidates into ws); fx_knn_reduce
+ * launches the merge that turns them into out_dist / out_row.  Both must be
+ * given the same arguments.
+ * Batched queries (nq >= 8, float32, inner product / cosine) take the MFMA
+ * path: fx_knn_scan runs the sampled-threshold GEMM phases and fx_knn_reduce
+ * synchronises the stream once to recompute any query whose candidates
+ * overflowed (exact single-query scan), so it is not graph-capturable.
  */
 int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
                 const float* queries, int64_t nq, int metric, int64_t k,
                 const uint32_t* mask, void* ws, size_t ws_bytes, void* stream);
-int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t nq, int metric,
-                  int64_t k, void* ws, size_t ws_bytes, float* out_dist, int64_t* out_row,
-                  void* stream);
+int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                  const float* queries, int64_t nq, int metric, int64_t k,
+                  const uint32_t* mask, void* ws, size_t ws_bytes, float* out_dist,
+                  int64_t* out_row, void* stream);
 
 /*
  * All distances of nq queries to every corpus row: out[nq][n] float32.

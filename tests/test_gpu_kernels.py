@@ -298,3 +298,70 @@ def test_error_paths(eng):
         eng.search([Shard(x, 0)], q, 0, _lib.max_k() + 1)
     with pytest.raises(ValueError):
         eng.search([Shard(x, 0)], q, 7, 5)
+
+
+# ------------------------------------------------------------ batched (MFMA)
+
+
+@pytest.mark.parametrize("n,d,nq,k", [
+    (1000, 64, 8, 10),          # n <= cap: one phase, no threshold
+    (50_000, 128, 64, 10),
+    (300_000, 768, 256, 100),   # three sampled phases
+    (200_000, 96, 300, 1000),   # two query tiles, k = 1000
+    (70_001, 36, 9, 33),        # ragged tail tile, d not a multiple of 32
+])
+@pytest.mark.parametrize("metric", ["inner_product", "cosine"])
+def test_batched_mfma_parity(eng, n, d, nq, k, metric):
+    x = gpu_fill(eng, n, d, seed=n % 97)
+    xh = O.fill_normal(n, d, n % 97)
+    q = O.fill_normal(nq, d, seed=5)
+    gd, gr = gpu_search(eng, x, q, metric, k)
+    od, orow = O.knn(xh, q, metric, k)
+    check_topk(gd, gr, od, orow, xh, q, metric)
+
+
+def test_batched_masked_and_clustered(eng):
+    n, d, nq, k = 120_000, 256, 32, 50
+    x = gpu_fill(eng, n, d, seed=3, cluster=1000)
+    xh = O.fill_normal(n, d, 3, cluster=1000)
+    q = O.fill_normal(nq, d, seed=4, cluster=0)
+    q[:8] = xh[[5, 1500, 77_777, 119_999, 2, 3, 4, 60_000]]  # queries inside clusters
+    mask = np.random.RandomState(7).rand(n) < 0.3
+    for metric in ("inner_product", "cosine"):
+        gd, gr = gpu_search(eng, x, q, metric, k, mask=mask, row_base=17)
+        od, orow = O.knn(xh, q, metric, k, mask=mask, row_base=17)
+        check_topk(gd, gr, od, orow, xh, q, metric)
+
+
+def test_batched_overflow_fallback(eng, monkeypatch):
+    """Queries whose final candidates overflow are recomputed by the exact
+    single-query scan: forced for every query, results must not change."""
+    n, d, nq, k = 40_000, 128, 16, 20
+    x = gpu_fill(eng, n, d, seed=9)
+    xh = O.fill_normal(n, d, 9)
+    q = O.fill_normal(nq, d, seed=10)
+    base_d, base_r = gpu_search(eng, x, q, "cosine", k)
+    monkeypatch.setenv("FX_BATCH_FORCE_FALLBACK", "1")
+    fd, fr = gpu_search(eng, x, q, "cosine", k)
+    od, orow = O.knn(xh, q, "cosine", k)
+    check_topk(fd, fr, od, orow, xh, q, "cosine")
+    check_topk(base_d, base_r, od, orow, xh, q, "cosine")
+    monkeypatch.setenv("FX_BATCH_FORCE_FALLBACK", "0")
+    monkeypatch.setenv("FX_BATCH_CAP", str(16 * k))  # tiny buffers: more phases
+    sd, sr = gpu_search(eng, x, q, "cosine", k)
+    check_topk(sd, sr, od, orow, xh, q, "cosine")
+
+
+def test_batched_equals_unbatched(eng, monkeypatch):
+    """The MFMA path and the per-query scan agree (ids; distances to f32 rounding)."""
+    n, d, nq, k = 100_000, 768, 24, 100
+    x = gpu_fill(eng, n, d, seed=11)
+    q = O.fill_normal(nq, d, seed=12)
+    bd, br = gpu_search(eng, x, q, "cosine", k)
+    monkeypatch.setenv("FX_BATCH", "0")
+    sd, sr = gpu_search(eng, x, q, "cosine", k)
+    xh = O.fill_normal(n, d, 11)
+    od, orow = O.knn(xh, q, "cosine", k)
+    check_topk(bd, br, od, orow, xh, q, "cosine")
+    check_topk(sd, sr, od, orow, xh, q, "cosine")
+    assert np.max(np.abs(bd - sd)) <= 1e-6

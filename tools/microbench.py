@@ -28,7 +28,7 @@ def bind(path):
     i64, sz, vp, ci = ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
     L.fx_knn_workspace_bytes.argtypes = [i64, i64, ci, i64, i64, ctypes.POINTER(sz)]
     L.fx_knn_scan.argtypes = [vp, ci, i64, i64, i64, vp, i64, ci, i64, vp, vp, sz, vp]
-    L.fx_knn_reduce.argtypes = [vp, ci, i64, i64, i64, ci, i64, vp, sz, vp, vp, vp]
+    L.fx_knn_reduce.argtypes = [vp, ci, i64, i64, i64, vp, i64, ci, i64, vp, vp, sz, vp, vp, vp]
     L.fx_last_error.restype = ctypes.c_char_p
     return L
 
@@ -127,7 +127,7 @@ def main():
         else:
             os.environ.pop("FX_MERGE_GROUP", None)
         ws = eng.scan(shard, q, a.metric, k)
-        ts = timed(lambda: eng.reduce(shard, 1, a.metric, k, ws, od, orow), a.iters * 2)
+        ts = timed(lambda: eng.reduce(shard, q, a.metric, k, ws, od, orow), a.iters * 2)
         results[f"reduce[group={g or 'auto'}]"] = ts
     os.environ.pop("FX_MERGE_GROUP", None)
 
