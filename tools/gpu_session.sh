@@ -25,6 +25,8 @@ for step in "$@"; do
     testk) run pytest_kernels 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_fullsize.py -m gpu -q -x -p no:cacheprovider ;;
     testsall) run pytest_gpu 1500 python -u -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python -u bench.py ;;
+    bench3) run bench3 900 python -u bench.py --nq 256 --metric cosine --steps 5 --warmup 1 --no-cpu-baseline ;;
+    prof3) run prof3 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 -u bench.py --nq 256 --metric cosine --steps 3 --warmup 1 --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc -o run --output-format csv -- python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     micro) run microbench 900 python -u tools/microbench.py --occ 0,2 --groups 0,8,16,32,64 ;;
