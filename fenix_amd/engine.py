@@ -138,36 +138,74 @@ class Shard:
 
 
 @dataclass
+class Piece:
+    """The part of one staged column that lives on one device."""
+
+    device: torch.device
+    data: torch.Tensor  # [rows, D]
+    start: int  # first row of the column held here
+
+
+@dataclass
 class _Entry:
     key: tuple
     table: pa.Table
-    shard_data: torch.Tensor
-    offsets: Dict[str, np.ndarray] = field(default_factory=dict)
+    pieces: List[Piece]
+
+
+def devices() -> List[torch.device]:
+    """Devices a server process shards its corpora over.
+
+    ``FENIX_AMD_DEVICES``: comma-separated ordinals, or ``all``; default: the
+    current device only.  Repeating an ordinal (``0,0``) is allowed and makes
+    several shards share one GPU (used to exercise the multi-device path on a
+    single-GPU machine)."""
+    require_gpu()
+    env = os.environ.get("FENIX_AMD_DEVICES", "").strip()
+    if env == "all":
+        return [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
+    if env:
+        return [torch.device("cuda", int(v)) for v in env.split(",") if v.strip()]
+    single = os.environ.get("FENIX_AMD_DEVICE")
+    return [torch.device("cuda", int(single) if single else torch.cuda.current_device())]
+
+
+def stage_sharded(col: pa.ChunkedArray, devs: Sequence[torch.device]) -> List[Piece]:
+    """Row-range shards of one column over ``devs`` (SURVEY §8(e) partitioning)."""
+    from .distributed import shard_rows
+
+    pieces = []
+    for i, dev in enumerate(devs):
+        start, count = shard_rows(len(col), len(devs), i)
+        with torch.cuda.device(dev):
+            pieces.append(Piece(dev, stage_column(col.slice(start, count), dev), start))
+    return pieces
 
 
 class CorpusCache:
-    """HBM-resident embedding columns keyed by (path, size, mtime_ns, column, device)."""
+    """HBM-resident embedding columns keyed by (path, size, mtime_ns, column, devices)."""
 
     def __init__(self) -> None:
         self._lock = threading.Lock()
         self._entries: Dict[tuple, _Entry] = {}
 
     @staticmethod
-    def _key(path: str, column: str, device: torch.device) -> tuple:
+    def _key(path: str, column: str, devs: Sequence[torch.device]) -> tuple:
         st = os.stat(path)
-        return (os.path.abspath(path), st.st_size, st.st_mtime_ns, column, str(device))
+        return (os.path.abspath(path), st.st_size, st.st_mtime_ns, column,
+                tuple(str(d) for d in devs))
 
-    def get(self, path: str, table: pa.Table, column: str, device: torch.device) -> _Entry:
-        key = self._key(path, column, device)
+    def get(self, path: str, table: pa.Table, column: str,
+            devs: Sequence[torch.device]) -> _Entry:
+        key = self._key(path, column, devs)
         with self._lock:
             hit = self._entries.get(key)
             if hit is not None:
                 return hit
-            # drop stale versions of the same file/column/device
+            # drop stale versions of the same file/column/devices
             for k in [k for k in self._entries if k[0] == key[0] and k[3:] == key[3:]]:
                 del self._entries[k]
-            data = stage_column(table.column(column), device)
-            entry = _Entry(key, table, data)
+            entry = _Entry(key, table, stage_sharded(table.column(column), devs))
             self._entries[key] = entry
             return entry
 
@@ -328,3 +366,48 @@ def device_mask(mask: Optional[np.ndarray], device: torch.device) -> Optional[to
         return None
     words = bitmap(mask)
     return torch.from_numpy(words.view(np.int32)).to(device)
+
+
+def search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: int,
+               masks: Optional[Sequence[Optional[torch.Tensor]]] = None
+               ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Exact top-k over shards that may live on several devices.
+
+    Each device's shards are searched by that device's Engine (all launches are
+    asynchronous, so the devices scan concurrently); the per-device [nq, k]
+    results are copied to the first device (peer-to-peer over xGMI, a few KB)
+    and merged there by fx_topk_merge.  Single process: the gather is a copy,
+    not a collective (the one-process-per-GPU path uses RCCL, distributed.py).
+    """
+    groups: Dict[torch.device, List[int]] = {}
+    for i, s in enumerate(shards):
+        groups.setdefault(s.data.device, []).append(i)
+    per = []
+    for dev, idx in groups.items():
+        with torch.cuda.device(dev):
+            eng = Engine.get(dev)
+            ms = [masks[i] for i in idx] if masks is not None else None
+            per.append(eng.search([shards[i] for i in idx], queries, metric, k, ms))
+    if len(per) == 1:
+        return per[0]
+    dev0 = next(iter(groups))
+    with torch.cuda.device(dev0):
+        eng0 = Engine.get(dev0)
+        dd = torch.stack([d.to(dev0) for d, _ in per], dim=1)
+        rr = torch.stack([r.to(dev0) for _, r in per], dim=1)
+        with eng0.lock:
+            return eng0.merge(dd, rr, k)
+
+
+def distances_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int,
+                  masks: Optional[Sequence[Optional[torch.Tensor]]] = None) -> np.ndarray:
+    """[nq, sum of shard rows] distances, shards concatenated in order."""
+    outs = []
+    for i, s in enumerate(shards):
+        dev = s.data.device
+        with torch.cuda.device(dev):
+            m = masks[i] if masks is not None else None
+            outs.append(Engine.get(dev).distances(s, queries, metric, m))
+    if not outs:
+        return np.zeros((queries.shape[0], 0), np.float32)
+    return np.concatenate([o.cpu().numpy() for o in outs], axis=1)

@@ -109,15 +109,16 @@ def take_rows(data: pa.Table, rows: np.ndarray) -> pa.Table:
     return pa.Table.from_arrays(cols, schema=data.schema)
 
 
-def _shards(parts, column: str, device: torch.device):
+def _shards(parts, column: str, devs):
+    """HBM shards of every source, row-range split over ``devs``; global rows
+    continue across sources in order (table.py:19-21)."""
     shards, base = [], 0
     for path, t in parts:
         if path is not None:
-            entry = _engine.CACHE.get(path, t, column, device)
-            data = entry.shard_data
+            pieces = _engine.CACHE.get(path, t, column, devs).pieces
         else:
-            data = _engine.stage_column(t.column(column), device)
-        shards.append(_engine.Shard(data, base))
+            pieces = _engine.stage_sharded(t.column(column), devs)
+        shards.extend(_engine.Shard(p.data, base + p.start) for p in pieces if p.data.shape[0])
         base += t.num_rows
     return shards
 
@@ -154,28 +155,23 @@ def call(
     mask = _filter_mask(data, filter) if filter is not None else None
     n_rows = int(mask.sum()) if mask is not None else data.num_rows
 
-    eng = _engine.Engine.get()
-    shards = _shards(parts, column, eng.device)
+    shards = _shards(parts, column, _engine.devices())
     masks = None
     if mask is not None:
-        masks = [_engine.device_mask(mask[s.row_base : s.row_base + s.n], eng.device)
+        masks = [_engine.device_mask(mask[s.row_base : s.row_base + s.n], s.data.device)
                  for s in shards]
     qt = torch.from_numpy(q)
     base_cols = [c for c in dict.fromkeys(select) if c != DIST_COL]
 
     if maxval is not None and n_rows > maxval:
-        dist, rows = eng.search(shards, qt, m, int(maxval), masks)
+        dist, rows = _engine.search_all(shards, qt, m, int(maxval), masks)
         dist = dist[0].cpu().numpy()
         rows = rows[0].cpu().numpy()
         keep = rows >= 0
         dist, rows = dist[keep], rows[keep]
         out = take_rows(data.select(base_cols), rows)
     else:
-        dists = []
-        for i, s in enumerate(shards):
-            dm = masks[i] if masks is not None else None
-            dists.append(eng.distances(s, qt, m, dm)[0].cpu().numpy())
-        dist = np.concatenate(dists) if dists else np.zeros(0, np.float32)
+        dist = _engine.distances_all(shards, qt, m, masks)[0]
         out = data.select(base_cols)
         if mask is not None:
             out = out.filter(pa.array(mask))

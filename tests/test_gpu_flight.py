@@ -181,6 +181,28 @@ def test_table_source_and_coder_distance(env):
         assert np.all(np.abs(got - ref) <= 1e-5 * scale)
 
 
+def test_sharded_over_devices(env, monkeypatch):
+    """FENIX_AMD_DEVICES row-shards the staged column (here 3 shards on one GPU;
+    on a node, one per GPU); results are identical to the unsharded search."""
+    root = env["root"]
+    t = O.fill_normal(1, VECTOR_SIZE, seed=34)[0]
+    base = index.call(root, None, "test/table", "vector", target=t, metric="l2", maxval=100)
+    monkeypatch.setenv("FENIX_AMD_DEVICES", "0,0,0")
+    sh = index.call(root, None, "test/table", "vector", target=t, metric="l2", maxval=100)
+    assert sh.equals(base)
+    expr = pc.field("id") >= 50_000
+    sf = index.call(root, None, ["test/table", "test/table"], "vector", target=t,
+                    metric="cosine", filter=expr, maxval=30)
+    both = np.concatenate([env["x"], env["x"]])
+    mask = np.concatenate([np.arange(NUM_VECTORS) >= 50_000] * 2)
+    od, orow = O.knn(both, t[None], "cosine", 30, mask=mask)
+    vec = np.stack(sf.column("vector").to_numpy(zero_copy_only=False))
+    np.testing.assert_array_equal(vec, both[orow[0]])
+    full = index.call(root, None, "test/table", "vector", target=t, metric="dot", select=["id"])
+    ref = O.distances(env["x"], t[None], "dot")[0]
+    assert np.all(np.abs(full.column("__DISTANCE__").to_numpy() - ref) <= 1e-5 * np.abs(ref).max())
+
+
 def test_remove(env):
     flight = env["flight"]
     flight.remove()
