@@ -34,7 +34,6 @@ import pyarrow as pa
 import pyarrow.compute as pc
 import pyarrow.flight as fl
 from pydantic.dataclasses import dataclass
-from torch import Tensor
 from typing_extensions import Self
 
 from . import io
@@ -209,7 +208,7 @@ class Flight:
 
     def search(
         self,
-        target: pa.Array | pa.ChunkedArray | pa.FixedSizeListScalar | np.ndarray | Tensor,
+        target,  # pa.Array | pa.ChunkedArray | pa.FixedSizeListScalar | np.ndarray | Tensor
         source: str | Sequence[str],
         column: str,
         metric: str,
@@ -238,7 +237,7 @@ class Flight:
             )
         )
 
-        if isinstance(target, Tensor):
+        if type(target).__module__.split(".")[0] == "torch":  # Tensor, without importing torch
             target = target.numpy()
 
         if isinstance(target, np.ndarray):

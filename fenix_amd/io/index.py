@@ -35,7 +35,9 @@ approximate search outside the MI355X hot path and raises
 
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+import os
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import pyarrow as pa
@@ -44,19 +46,43 @@ import torch
 from torch import Tensor
 
 from .. import engine as _engine
-from . import coder, table
+from . import arrow, coder, table
 
 CODE_COL: str = "__CODED_ID__"
 DIST_COL: str = "__DISTANCE__"
 LOCATION: str = "indexes"
 
 
-def _sources(root: str, source) -> Tuple[pa.Table, List[Tuple[Optional[str], pa.Table]]]:
+_lock = threading.Lock()
+_TABLES: Dict[str, Tuple[tuple, pa.Table]] = {}  # path -> (stat key, mmap'd table)
+_COMBINED: Dict[tuple, pa.Array] = {}  # (stat keys, column) -> single-chunk column
+
+
+def _load(path: str) -> Tuple[tuple, pa.Table]:
+    """io.arrow.load (arrow.py:6-8) once per file version: the mmap'd table is
+    reused while (size, mtime) are unchanged; do_put rewrites invalidate it."""
+    st = os.stat(path)
+    key = (os.path.abspath(path), st.st_size, st.st_mtime_ns)
+    with _lock:
+        hit = _TABLES.get(key[0])
+        if hit is not None and hit[0] == key:
+            return hit
+    t = arrow.load(path)
+    with _lock:
+        _TABLES[key[0]] = (key, t)
+        for k in [k for k in _COMBINED if key[0] in (s[0] for s in k[0]) and key not in k[0]]:
+            del _COMBINED[k]
+    return key, t
+
+
+def _sources(root: str, source):
+    """-> (joined table, [(path or None, table)], version key or None)."""
     if isinstance(source, pa.Table):
-        return source, [(None, source)]
+        return source, [(None, source)], None
     names = [source] if isinstance(source, str) else list(source)
-    parts = [(table.path(root, n), table.load(root, n)) for n in names]
-    return table.join(*[t for _, t in parts]), parts
+    loaded = [(table.path(root, n),) + _load(table.path(root, n)) for n in names]
+    parts = [(p, t) for p, _, t in loaded]
+    return table.join(*[t for _, t in parts]), parts, tuple(k for _, k, _ in loaded)
 
 
 def _target_values(target, type: pa.DataType) -> np.ndarray:
@@ -109,6 +135,45 @@ def take_rows(data: pa.Table, rows: np.ndarray) -> pa.Table:
     return pa.Table.from_arrays(cols, schema=data.schema)
 
 
+def _gather_vectors(shards, rows: np.ndarray, type: pa.DataType) -> pa.Array:
+    """The k winning embeddings, read back from their HBM shards (they are the
+    stored Arrow values, staged verbatim) instead of gathered from Arrow
+    chunks: a few KB over PCIe instead of k chunk lookups."""
+    d = type.list_size
+    _, tdt, ndt = _engine.value_dtype(type)
+    out = np.empty((rows.size, d), dtype=ndt)
+    for s in shards:
+        sel = np.nonzero((rows >= s.row_base) & (rows < s.row_base + s.n))[0]
+        if sel.size:
+            idx = torch.from_numpy(rows[sel] - s.row_base).to(s.data.device)
+            out[sel] = s.data.index_select(0, idx).cpu().numpy()
+    return pa.FixedSizeListArray.from_arrays(pa.array(out.ravel()), list_size=d).cast(type)
+
+
+def _take_columns(data: pa.Table, cols: List[str], rows: np.ndarray, column: str, shards,
+                  version) -> pa.Table:
+    """select(cols).take(rows) without Table.take's concatenation of the whole
+    chunked vector column (index.py:166; 0.75 s per 1M x 768 measured)."""
+    arrays = []
+    for c in cols:
+        col = data.column(c)
+        if c == column and col.null_count == 0:
+            arrays.append(_gather_vectors(shards, rows, col.type))
+            continue
+        if version is None:
+            arrays.append(_take_chunked(col, rows))
+            continue
+        key = (version, c)
+        with _lock:
+            comb = _COMBINED.get(key)
+        if comb is None:
+            comb = col.combine_chunks()
+            with _lock:
+                _COMBINED[key] = comb
+        arrays.append(comb.take(pa.array(rows)))
+    return pa.Table.from_arrays(arrays, schema=data.select(cols).schema)
+
+
 def _shards(parts, column: str, devs):
     """HBM shards of every source, row-range split over ``devs``; global rows
     continue across sources in order (table.py:19-21)."""
@@ -140,7 +205,7 @@ def call(
             "coded-index (product-quantised) search is outside the fenix_amd brute-force path"
         )
 
-    data, parts = _sources(root, source)
+    data, parts, version = _sources(root, source)
     type = data.schema.field(column).type
     q = _target_values(target, type)
 
@@ -169,7 +234,7 @@ def call(
         rows = rows[0].cpu().numpy()
         keep = rows >= 0
         dist, rows = dist[keep], rows[keep]
-        out = take_rows(data.select(base_cols), rows)
+        out = _take_columns(data, base_cols, rows, column, shards, version)
     else:
         dist = _engine.distances_all(shards, qt, m, masks)[0]
         out = data.select(base_cols)

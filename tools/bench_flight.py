@@ -1,10 +1,13 @@
-"""End-to-end latency of Flight.search against a fenix_amd.Server (loopback).
+"""End-to-end latency of Flight.search against a fenix_amd.Server.
 
 Not the headline metric (bench.py is); this measures what a fenix client sees:
-descriptor pickling, gRPC DoExchange, io.index.call on the GPU, the k-row
-gather and the result stream.  Corpus written as an Arrow IPC stream of
-1 000-row batches like the reference's tests (test_flight.py:17-35); the first
-search stages the column into HBM and is reported separately.
+descriptor pickling, gRPC DoExchange over loopback, io.index.call on the GPU,
+the k-row gather and the result stream.  The server runs in this process; the
+client runs in a child process that does not import torch (a torch import in
+a client process alone costs ~10 ms per Flight round trip).  The
+corpus is written through Flight.make_table as 1 000-row batches like the
+reference's tests (test_flight.py:17-35); the first search stages the column
+into HBM and is reported separately.
 
     python tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2
     python tools/bench_flight.py --n 1000000 --d 1536 --k 1000 --metric inner_product --dtype f16
@@ -16,6 +19,7 @@ import argparse
 import json
 import os
 import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -25,10 +29,33 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 import pyarrow as pa  # noqa: E402
-import torch  # noqa: E402
 
 
-def main():
+def client(a) -> None:
+    """Child process: no torch, only the Flight client."""
+    import fenix_amd
+
+    assert "torch" not in sys.modules
+    f = fenix_amd.Flight(host="127.0.0.1", port=a.port)
+    rs = np.random.RandomState(1)
+    qs = rs.standard_normal((a.reps + 1, a.d)).astype(np.float16 if a.dtype == "f16" else np.float32)
+    t0 = time.perf_counter()
+    r = f.search(target=qs[0], source="bench/table", column="vector", metric=a.metric,
+                 maxval=a.k)
+    first = time.perf_counter() - t0
+    assert r.num_rows == a.k
+    lat = []
+    for i in range(a.reps):
+        t0 = time.perf_counter()
+        r = f.search(target=qs[i + 1], source="bench/table", column="vector", metric=a.metric,
+                     maxval=a.k)
+        lat.append(time.perf_counter() - t0)
+        assert r.num_rows == a.k
+    print(json.dumps({"first_ms": first * 1e3, "lat_ms": [v * 1e3 for v in lat],
+                      "torch_imported": "torch" in sys.modules}), flush=True)
+
+
+def main() -> None:
     p = argparse.ArgumentParser()
     p.add_argument("--n", type=int, default=100_000)
     p.add_argument("--d", type=int, default=128)
@@ -36,8 +63,14 @@ def main():
     p.add_argument("--metric", default="l2")
     p.add_argument("--dtype", default="f32", choices=["f32", "f16"])
     p.add_argument("--batch", type=int, default=1000)
-    p.add_argument("--reps", type=int, default=20)
+    p.add_argument("--reps", type=int, default=30)
+    p.add_argument("--client", action="store_true")
+    p.add_argument("--port", type=int, default=0)
     a = p.parse_args()
+    if a.client:
+        return client(a)
+
+    import torch
 
     import fenix_amd
     from fenix_amd.engine import Engine
@@ -62,37 +95,32 @@ def main():
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     server = fenix_amd.Server(root, host="127.0.0.1", port=port)
-    client = fenix_amd.Flight(host="127.0.0.1", port=port)
+    writer = fenix_amd.Flight(host="127.0.0.1", port=port)
     t0 = time.perf_counter()
-    client.make_table("bench/table", pa.RecordBatchReader.from_batches(schema, batches()))
+    writer.make_table("bench/table", pa.RecordBatchReader.from_batches(schema, batches()))
     t_put = time.perf_counter() - t0
-    qdev = torch.empty((a.reps + 1, a.d), dtype=torch.float32, device=eng.device)
-    eng.fill(qdev, seed=1)
-    qs = qdev.cpu().numpy().astype(np.float16 if a.dtype == "f16" else np.float32)
-    t0 = time.perf_counter()
-    r = client.search(target=qs[0], source="bench/table", column="vector", metric=a.metric,
-                      maxval=a.k)
-    t_first = time.perf_counter() - t0
-    assert r.num_rows == a.k
-    lat = []
-    for i in range(a.reps):
-        t0 = time.perf_counter()
-        r = client.search(target=qs[i + 1], source="bench/table", column="vector",
-                          metric=a.metric, maxval=a.k)
-        lat.append(time.perf_counter() - t0)
-        assert r.num_rows == a.k
+    cmd = [sys.executable, os.path.abspath(__file__), "--client", "--port", str(port),
+           "--d", str(a.d), "--k", str(a.k), "--metric", a.metric, "--dtype", a.dtype,
+           "--reps", str(a.reps)]
+    proc = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     server.shutdown()
+    if proc.returncode != 0:
+        print(proc.stderr, file=sys.stderr)
+        raise SystemExit(proc.returncode)
+    res = json.loads(proc.stdout.strip().splitlines()[-1])
+    lat = np.array(res["lat_ms"])
     med = float(np.median(lat))
-    out = {
-        "workload": f"{a.n}x{a.d} {a.dtype} {a.metric} k={a.k} via Flight.search (loopback)",
-        "median_ms": med * 1e3,
-        "p90_ms": float(np.percentile(lat, 90)) * 1e3,
-        "vectors_per_s": a.n / med,
-        "first_search_ms_incl_staging": t_first * 1e3,
+    print(json.dumps({
+        "workload": f"{a.n}x{a.d} {a.dtype} {a.metric} k={a.k} via Flight.search "
+                    "(loopback, torch-free client process)",
+        "median_ms": med,
+        "p90_ms": float(np.percentile(lat, 90)),
+        "vectors_per_s": a.n / (med * 1e-3),
+        "first_search_ms_incl_staging": res["first_ms"],
         "make_table_s": t_put,
         "reps": a.reps,
-    }
-    print(json.dumps(out), flush=True)
+        "client_imported_torch": res["torch_imported"],
+    }), flush=True)
 
 
 if __name__ == "__main__":
