@@ -21,7 +21,7 @@ struct ScanArgs {
   int cap;                // per-wave candidate list capacity
   size_t qbytes;          // LDS bytes reserved for the query
   int mode;               // kModeTopk / kModeDist
-  uint64_t* out_lists;    // topk: [nq][gridDim.x*4][k] composites
+  uint64_t* out_lists;    // topk: [nq][gridDim.x][k] composites (one list per block)
   float* out_dist;        // dist: [nq][n]
 };
 

@@ -23,7 +23,7 @@
 #include <stdlib.h>
 
 #include "fx_internal.h"
-#include "fx_wave.h"
+#include "fx_select.h"
 
 // Rows in flight per 16-lane group (U) for each slot count L (slots of 16 B
 // per lane per row pass).  Tuning knobs for tools/microbench.py variant builds.
@@ -403,9 +403,34 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanArgs a) {
     const uint64_t kth = wave_select(c.buf, cnt, a.k, c.hist, lane, &quota);
     cnt = wave_compact(c.buf, cnt, kth, quota, lane);
   }
-  uint64_t* out =
-      a.out_lists + ((size_t)qi * gridDim.x * 4 + (size_t)blockIdx.x * 4 + wid) * (size_t)a.k;
-  for (int i = lane; i < a.k; i += kWave) out[i] = i < cnt ? c.buf[i] : kEmpty;
+  // Fold the block's 4 wave lists (k each, padded) into one list of k:
+  // a quarter of the candidates for the merge kernels (block-wide select).
+  constexpr int kMaxPerLane = 16;  // k <= 1024
+  uint64_t mine[kMaxPerLane];
+#pragma unroll
+  for (int j = 0; j < kMaxPerLane; ++j) {
+    const int i = lane + j * kWave;
+    mine[j] = i < cnt ? c.buf[i] : kEmpty;
+  }
+  __syncthreads();
+  uint64_t* all = reinterpret_cast<uint64_t*>(smem + a.qbytes);  // 4k entries fit in 4 caps
+  uint64_t v_or = 0, v_and = ~0ull;
+#pragma unroll
+  for (int j = 0; j < kMaxPerLane; ++j) {
+    const int i = lane + j * kWave;
+    if (i < a.k) {
+      all[wid * a.k + i] = mine[j];
+      v_or |= mine[j];
+      v_and &= mine[j];
+    }
+  }
+  MergeShared* ms = reinterpret_cast<MergeShared*>(smem + a.qbytes + (size_t)4 * a.cap * 8);
+  block_reset(ms);
+  __syncthreads();
+  block_or_and(v_or, v_and, ms);
+  __syncthreads();
+  uint64_t* out = a.out_lists + ((size_t)qi * gridDim.x + blockIdx.x) * (size_t)a.k;
+  block_keep_k(all, 4 * a.k, a.k, out, ms);
 }
 
 // ----------------------------------------------------- dispatch / planning --
@@ -536,7 +561,7 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   if (blocks < 1) blocks = 1;
   p->blocks = blocks;
   p->rows_per_block = rpb > 0 ? rpb : step;
-  p->nlists = blocks * 4;
+  p->nlists = blocks;  // one list per block (the epilogue folds its 4 waves)
   return FX_OK;
 }
 
