@@ -1,4 +1,4 @@
-// Block-wide (256-thread) selection of the k smallest 64-bit composites held
+// Block-wide (NT-thread, NT >= 256) selection of the k smallest 64-bit composites held
 // in LDS — shared by the merge kernel and the scan kernel's epilogue.
 #pragma once
 
@@ -18,6 +18,7 @@ struct MergeShared {
 // k-th smallest of s[0..m) (m > k).  start_shift: the byte holding the
 // highest bit in which the entries differ (higher bytes are common to all,
 // so their passes would put every entry in one bin).
+template <int NT>
 __device__ __forceinline__ uint64_t block_select(const uint64_t* s, int m, int k,
                                                  int start_shift, uint64_t common,
                                                  MergeShared* ms, int* quota_eq) {
@@ -27,12 +28,20 @@ __device__ __forceinline__ uint64_t block_select(const uint64_t* s, int m, int k
   uint64_t prefix = common & pmask;
   uint32_t need = (uint32_t)k;
   for (int shift = start_shift; shift >= 0; shift -= 8) {
-    ms->hist[tid] = 0u;
+    if (tid < 256) ms->hist[tid] = 0u;
     __syncthreads();
-    for (int base = wid * kWave; base < m; base += kBlockThreads) {
-      const int i = base + lane;
-      const uint64_t e = i < m ? s[i] : kEmpty;
-      hist_add(ms->hist, (uint32_t)(e >> shift) & 255u, i < m && (e & pmask) == prefix);
+    for (int b0 = wid * kWave; b0 < m; b0 += 4 * NT) {
+      uint64_t e[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // 4 LDS reads in flight
+        const int i = b0 + u * NT + lane;
+        e[u] = i < m ? s[i] : kEmpty;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = b0 + u * NT + lane;
+        hist_add(ms->hist, (uint32_t)(e[u] >> shift) & 255u, i < m && (e[u] & pmask) == prefix);
+      }
     }
     __syncthreads();
     if (wid == 0) {
@@ -67,7 +76,7 @@ __device__ __forceinline__ uint64_t block_select(const uint64_t* s, int m, int k
     pmask |= 0xffull << shift;
     if (inbin == need) {
       uint64_t mx = 0;
-      for (int i = tid; i < m; i += kBlockThreads) {
+      for (int i = tid; i < m; i += NT) {
         const uint64_t e = s[i];
         if ((e & pmask) == prefix && e > mx) mx = e;
       }
@@ -76,7 +85,7 @@ __device__ __forceinline__ uint64_t block_select(const uint64_t* s, int m, int k
       __syncthreads();
       const uint64_t T = ms->shmax;
       int eq = 0;
-      for (int i = tid; i < m; i += kBlockThreads) eq += s[i] == T ? 1 : 0;
+      for (int i = tid; i < m; i += NT) eq += s[i] == T ? 1 : 0;
       eq = wave_sum_i(eq);
       if (lane == 0) atomicAdd(&ms->sh[3], (uint32_t)eq);
       __syncthreads();
@@ -116,15 +125,16 @@ __device__ __forceinline__ void block_or_and(uint64_t v_or, uint64_t v_and, Merg
 
 // Keep the k smallest of s[0..m) (m > k; all_or/all_and ready in ms): writes
 // exactly k entries, in no particular order, to dst[0..k) (LDS or global).
+template <int NT>
 __device__ __forceinline__ void block_keep_k(const uint64_t* s, int m, int k, uint64_t* dst,
                                              MergeShared* ms) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint64_t diff = ms->all_or ^ ms->all_and;
   const int start_shift = diff ? (63 - __clzll((long long)diff)) / 8 * 8 : 0;
   int quota;
-  const uint64_t T = block_select(s, m, k, start_shift, ms->all_and, ms, &quota);
+  const uint64_t T = block_select<NT>(s, m, k, start_shift, ms->all_and, ms, &quota);
   const uint64_t ltmask = (1ull << lane) - 1ull;
-  for (int base = wid * kWave; base < m; base += kBlockThreads) {
+  for (int base = wid * kWave; base < m; base += NT) {
     const int i = base + lane;
     const bool in_range = i < m;
     const uint64_t e = in_range ? s[i] : kEmpty;

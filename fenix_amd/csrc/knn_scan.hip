@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanArgs a) {
   block_or_and(v_or, v_and, ms);
   __syncthreads();
   uint64_t* out = a.out_lists + ((size_t)qi * gridDim.x + blockIdx.x) * (size_t)a.k;
-  block_keep_k(all, 4 * a.k, a.k, out, ms);
+  block_keep_k<256>(all, 4 * a.k, a.k, out, ms);
 }
 
 // ----------------------------------------------------- dispatch / planning --
