@@ -45,18 +45,25 @@ struct BatchShared {
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
+#ifndef FX_BATCH_WAVES
+#define FX_BATCH_WAVES 8  // 4: one wave per SIMD; 8: two (4 row groups x 2 query halves)
+#endif
+constexpr int kWaves = FX_BATCH_WAVES;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kQTiles = 8 * 4 / kWaves;  // 32-query MFMA tiles per wave
+
 // Stage one K chunk (columns [k0, k0+32)) of X rows [r0, r0+128) and of the
-// query tile into registers: X 4 x 16 B per thread, Q 8 x 16 B per thread.
+// query tile into registers (16-B pieces; 1024 of X, 2048 of Q per chunk).
 struct Prefetch {
-  f32x4 x[4];
-  f32x4 q[8];
+  f32x4 x[1024 / kThreads];
+  f32x4 q[2048 / kThreads];
 };
 
 __device__ __forceinline__ void prefetch_chunk(Prefetch& p, const BatchArgs& a, int64_t r0,
                                                int64_t q0, int k0, int tid) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int idx = i * 256 + tid;  // 0..1023: row = idx/8, col4 = idx%8
+  for (int i = 0; i < 1024 / kThreads; ++i) {
+    const int idx = i * kThreads + tid;  // row = idx/8, col4 = idx%8
     const int row = idx >> 3, c4 = idx & 7;
     const int64_t gr = r0 + row;
     const int k = k0 + c4 * 4;
@@ -68,8 +75,8 @@ __device__ __forceinline__ void prefetch_chunk(Prefetch& p, const BatchArgs& a, 
     }
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int idx = i * 256 + tid;  // 0..2047: query = idx/8, col4 = idx%8
+  for (int i = 0; i < 2048 / kThreads; ++i) {
+    const int idx = i * kThreads + tid;  // query = idx/8, col4 = idx%8
     const int qq = idx >> 3, c4 = idx & 7;
     const int64_t gq = q0 + qq;
     const int k = k0 + c4 * 4;
@@ -79,32 +86,34 @@ __device__ __forceinline__ void prefetch_chunk(Prefetch& p, const BatchArgs& a, 
 
 __device__ __forceinline__ void store_chunk(const Prefetch& p, BatchShared* sh, int buf, int tid) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int idx = i * 256 + tid;
+  for (int i = 0; i < 1024 / kThreads; ++i) {
+    const int idx = i * kThreads + tid;
     *reinterpret_cast<f32x4*>(&sh->xs[buf][(idx >> 3) * kLds + (idx & 7) * 4]) = p.x[i];
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int idx = i * 256 + tid;
+  for (int i = 0; i < 2048 / kThreads; ++i) {
+    const int idx = i * kThreads + tid;
     *reinterpret_cast<f32x4*>(&sh->qs[buf][(idx >> 3) * kLds + (idx & 7) * 4]) = p.q[i];
   }
 }
 
 template <int METRIC>
-__global__ void __launch_bounds__(256, 1) batch_kernel(BatchArgs a) {
+__global__ void __launch_bounds__(kThreads, 1) batch_kernel(BatchArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   BatchShared* sh = reinterpret_cast<BatchShared*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int rg = wid & 3;                   // 32-row group of this wave
+  const int qtile0 = (wid >> 2) * kQTiles;  // first 32-query tile of this wave
   const int h = lane >> 5, l32 = lane & 31;
   const int64_t q0 = (int64_t)blockIdx.y * kBQ;
   const int nchunks = (a.d + kBK - 1) / kBK;
 
-  // per-lane query state for its 8 query columns
-  uint64_t thr[8];
-  float qn[8];
+  // per-lane query state for its query columns
+  uint64_t thr[kQTiles];
+  float qn[kQTiles];
 #pragma unroll
-  for (int qt = 0; qt < 8; ++qt) {
-    const int64_t gq = q0 + qt * 32 + l32;
+  for (int qt = 0; qt < kQTiles; ++qt) {
+    const int64_t gq = q0 + (qtile0 + qt) * 32 + l32;
     thr[qt] = gq < a.nq ? a.thr[gq] : 0ull;
     qn[qt] = gq < a.nq ? a.qnorm[gq] : 1.f;
   }
@@ -114,9 +123,9 @@ __global__ void __launch_bounds__(256, 1) batch_kernel(BatchArgs a) {
     const int64_t r0 = tile * kBM;
     if (r0 >= a.n) continue;
 
-    f32x16 acc[8];
+    f32x16 acc[kQTiles];
 #pragma unroll
-    for (int qt = 0; qt < 8; ++qt) acc[qt] = f32x16(0.f);
+    for (int qt = 0; qt < kQTiles; ++qt) acc[qt] = f32x16(0.f);
     float sumsq = 0.f;
 
     Prefetch pf;
@@ -128,8 +137,8 @@ __global__ void __launch_bounds__(256, 1) batch_kernel(BatchArgs a) {
     for (int c = 0; c < nchunks; ++c) {
       const int buf = c & 1;
       if (c + 1 < nchunks) prefetch_chunk(pf, a, r0, q0, (c + 1) * kBK, tid);
-      const float* xs = sh->xs[buf] + (wid * 32 + l32) * kLds + 4 * h;
-      const float* qs = sh->qs[buf] + l32 * kLds + 4 * h;
+      const float* xs = sh->xs[buf] + (rg * 32 + l32) * kLds + 4 * h;
+      const float* qs = sh->qs[buf] + (qtile0 * 32 + l32) * kLds + 4 * h;
 #pragma unroll
       for (int g = 0; g < kBK / 8; ++g) {
         const f32x4 av = ld4(xs + 8 * g);
@@ -140,7 +149,7 @@ __global__ void __launch_bounds__(256, 1) batch_kernel(BatchArgs a) {
           sumsq = fmaf(av[3], av[3], sumsq);
         }
 #pragma unroll
-        for (int qt = 0; qt < 8; ++qt) {
+        for (int qt = 0; qt < kQTiles; ++qt) {
           const f32x4 bv = ld4(qs + qt * 32 * kLds + 8 * g);
 #pragma unroll
           for (int t = 0; t < 4; ++t)
@@ -154,19 +163,19 @@ __global__ void __launch_bounds__(256, 1) batch_kernel(BatchArgs a) {
     // ---- epilogue: distances, threshold filter, append
     if constexpr (METRIC == 2) {
       sumsq += __shfl_xor(sumsq, 32);
-      if (h == 0) sh->rownorm[wid * 32 + l32] = fmaxf(sqrtf(sumsq), 1e-12f);
+      if (h == 0 && qtile0 == 0) sh->rownorm[rg * 32 + l32] = fmaxf(sqrtf(sumsq), 1e-12f);
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int lr = wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int lr = rg * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
       const int64_t row = r0 + lr;
       bool ok = row < a.n;
       if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
       float nx = 1.f;
       if constexpr (METRIC == 2) nx = sh->rownorm[lr];
 #pragma unroll
-      for (int qt = 0; qt < 8; ++qt) {
+      for (int qt = 0; qt < kQTiles; ++qt) {
         const float dot = acc[qt][r];
         float dist;
         if constexpr (METRIC == 1) {
@@ -176,7 +185,7 @@ __global__ void __launch_bounds__(256, 1) batch_kernel(BatchArgs a) {
         }
         const uint64_t comp = make_comp(dist, (uint32_t)(a.row_base + row));
         if (ok && comp <= thr[qt]) {
-          const int64_t gq = q0 + qt * 32 + l32;
+          const int64_t gq = q0 + (qtile0 + qt) * 32 + l32;
           const uint32_t pos = atomicAdd(&a.count[gq], 1u);
           if (pos < (uint32_t)a.cap) a.cand[gq * a.cap + pos] = comp;
         }
@@ -213,7 +222,7 @@ int launch_batch(const BatchArgs& a, int metric, hipStream_t stream) {
     b.cand = a.cand + y0 * kBQ * (int64_t)a.cap;
     b.nq = a.nq - y0 * kBQ;
     void* args[] = {(void*)&b};
-    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(256), args, smem,
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(kThreads), args, smem,
                                    stream);
     if (e != hipSuccess) {
       set_error("batch_kernel launch: %s", hipGetErrorString(e));

@@ -55,6 +55,7 @@ def main():
     p.add_argument("--occ", default="0,2,3,4")
     p.add_argument("--groups", default="0,8,16,32")
     p.add_argument("--variants", action="store_true")
+    p.add_argument("--nq", type=int, default=1)
     p.add_argument("--sweep", default="", help="d:dtype list, e.g. 128:f32,1536:f16 (occ only)")
     a = p.parse_args()
     if a.sweep:
@@ -63,7 +64,8 @@ def main():
     n, d, k = a.n, a.d, a.k
     x = torch.empty((n, d), dtype=torch.float32, device=eng.device)
     eng.fill(x, seed=0)
-    q = torch.empty((1, d), dtype=torch.float32, device=eng.device)
+    nq = a.nq
+    q = torch.empty((nq, d), dtype=torch.float32, device=eng.device)
     eng.fill(q, seed=1)
     nbytes = n * d * 4
     stream = torch.cuda.current_stream().cuda_stream
@@ -77,7 +79,7 @@ def main():
     def scan_variant(L, occ):
         os.environ.pop("FX_SCAN_BLOCKS_PER_CU", None)  # max blocks = largest workspace
         need = ctypes.c_size_t(0)
-        assert L.fx_knn_workspace_bytes(n, d, 0, 1, k, ctypes.byref(need)) == 0
+        assert L.fx_knn_workspace_bytes(n, d, 0, nq, k, ctypes.byref(need)) == 0
         ws = torch.empty(need.value, dtype=torch.uint8, device=eng.device)
 
         def run():
@@ -85,7 +87,7 @@ def main():
                 os.environ["FX_SCAN_BLOCKS_PER_CU"] = str(occ)
             else:
                 os.environ.pop("FX_SCAN_BLOCKS_PER_CU", None)
-            rc = L.fx_knn_scan(x.data_ptr(), 0, n, d, 0, q.data_ptr(), 1, a.metric, k, None,
+            rc = L.fx_knn_scan(x.data_ptr(), 0, n, d, 0, q.data_ptr(), nq, a.metric, k, None,
                                ws.data_ptr(), ws.numel(), stream)
             assert rc == 0, L.fx_last_error()
         return run
@@ -105,7 +107,7 @@ def main():
     for name, L in bound.items():
         for occ in [int(v) for v in a.occ.split(",")]:
             variants[f"scan[{name},occ={occ or 'max'}]"] = scan_variant(L, occ)
-    for blocks in (1024, 2048, 4096, 8192):
+    for blocks in (1024, 2048, 4096, 8192) if nq == 1 else ():
         for nt in (0, 1):
             variants[f"stream_read[blocks={blocks},nt={nt}]"] = stream_variant(blocks, nt)
     for r in range(a.rounds):
@@ -118,6 +120,8 @@ def main():
     os.environ.pop("FX_SCAN_BLOCKS_PER_CU", None)
 
     # merge (reduce) settings on the default scan
+    if nq > 1:
+        a.groups = "0"
     shard = Shard(x, 0)
     od = torch.empty((1, k), dtype=torch.float32, device=eng.device)
     orow = torch.empty((1, k), dtype=torch.int64, device=eng.device)
@@ -136,6 +140,8 @@ def main():
         med = float(np.median(ts))
         entry = {"median_ms": med, "min_ms": float(np.min(ts))}
         if name.startswith(("scan", "stream")):
+            if nq > 1:
+                entry["TFLOPs_median"] = 2.0 * n * nq * d / (med * 1e-3) / 1e12
             entry["GBps_median"] = nbytes / (med * 1e-3) / 1e9
             entry["GBps_best"] = nbytes / (np.min(ts) * 1e-3) / 1e9
         summary[name] = entry
