@@ -7,7 +7,7 @@ shard, merge to the final sorted k, and for N > 1 the RCCL all-gather of the
 per-rank top-k plus the final merge (weak scaling: 10M rows per GPU, so N=8 is
 configs[3], 80M rows).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n ROWS] [--d D]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows ROWS] [--d D]
                     [--k K] [--nq Q] [--metric l2|cosine|inner_product]
                     [--dtype f32|f16] [--no-cpu-baseline]
 
@@ -41,13 +41,14 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--n", type=int, default=10_000_000, help="rows per GPU")
+    p.add_argument("--rows", dest="n", type=int, default=10_000_000, help="rows per GPU")
     p.add_argument("--d", type=int, default=768)
     p.add_argument("--k", type=int, default=100)
     p.add_argument("--nq", type=int, default=1)
     p.add_argument("--metric", default="l2")
     p.add_argument("--dtype", default="f32", choices=["f32", "f16"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
@@ -103,10 +104,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; --dist-backend gloo lets several ranks share one GPU
+    # (multi-rank rehearsal on a single-GPU box: RCCL refuses duplicate GPUs)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
+    gloo = args.dist_backend == "gloo"
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     from fenix_amd import _lib
     from fenix_amd.distributed import allgather_topk
@@ -137,7 +145,11 @@ def main():
             ev[i][1].record()
         eng.reduce(shard, q, metric, k, ws, od, orow)
         if world > 1:
-            gd, gr = allgather_topk(od, orow)
+            if gloo:
+                gd, gr = allgather_topk(od.cpu(), orow.cpu())
+                gd, gr = gd.to(device), gr.to(device)
+            else:
+                gd, gr = allgather_topk(od, orow)  # one RCCL all-gather over xGMI
             return eng.merge(gd, gr, k)
         return od, orow
 
@@ -157,7 +169,8 @@ def main():
     elapsed = time.perf_counter() - t0
     scan_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if world > 1:
-        t = torch.tensor([elapsed, scan_ms], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, scan_ms], dtype=torch.float64,
+                         device="cpu" if gloo else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, scan_ms = float(t[0]), float(t[1])
 
@@ -226,7 +239,8 @@ def main():
                 "k": k,
                 "queries": nq,
                 "metric": args.metric,
-                "parallelism": f"row-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+                "parallelism": f"row-shard x{world}"
+                + ((" + gloo all-gather" if gloo else " + RCCL all-gather") if world > 1 else ""),
             },
             "roofline": roof,
             "cpu_baseline": cpu,

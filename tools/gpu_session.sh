@@ -31,9 +31,10 @@ for step in "$@"; do
     pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc -o run --output-format csv -- python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     flight1) run flight1 600 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 ;;
     flight5) run flight5 900 python -u tools/bench_flight.py --n 1000000 --d 1536 --k 1000 --metric inner_product --dtype f16 --reps 10 ;;
-    bench5) run bench5 600 python -u bench.py --n 6250000 --d 1536 --k 1000 --metric inner_product --dtype f16 --steps 10 --warmup 2 --no-cpu-baseline ;;
-    prof5) run prof5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python3 -u bench.py --n 6250000 --d 1536 --k 1000 --metric inner_product --dtype f16 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    bench5) run bench5 600 python -u bench.py --rows 6250000 --d 1536 --k 1000 --metric inner_product --dtype f16 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    prof5) run prof5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python3 -u bench.py --rows 6250000 --d 1536 --k 1000 --metric inner_product --dtype f16 --steps 10 --warmup 2 --no-cpu-baseline ;;
     microb) run microb 900 python -u tools/microbench.py --nq 256 --metric 2 --occ 0 --rounds 2 --iters 3 ;;
+    benchw2) run benchw2 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 1 --rows 2000000 --dist-backend gloo ;;
     micro) run microbench 900 python -u tools/microbench.py --occ 0,2 --groups 0,8,16,32,64 ;;
     sweep) run sweep 900 python -u tools/microbench.py --sweep 128:f32,256:f32,768:f32,1536:f32,768:f16,1536:f16 --occ 0,1,2,3,4 --rounds 2 --iters 6 ;;
     vsweep) run vsweep 1100 python -u tools/microbench.py --variants --sweep 768:f32,128:f32,256:f32,768:f16,1536:f16,1536:f32,100:f32 --occ 0,2 --rounds 2 --iters 5 ;;
