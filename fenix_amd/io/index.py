@@ -188,6 +188,42 @@ def _shards(parts, column: str, devs):
     return shards
 
 
+def register_distance(metric: str, type: pa.DataType) -> str:
+    """Register (once) the pyarrow scalar UDF ``distance:{metric}:{T}:{D}``.
+
+    The reference registers it lazily inside ``call`` (index.py:133-159):
+    ``(x: fixed_size_list<T>[D] array, q: same-type scalar) -> T array``, one
+    ``coder.distance`` per Arrow chunk.  ``call`` here does not need it (the
+    scan fuses distance + top-k), but code that invokes the function through
+    ``pc.call_function`` keeps working: each chunk is evaluated by the GPU
+    distance kernel (fx_knn_distances).  Returns the function name.
+    """
+    coder.metric_id(metric)
+    _engine.value_dtype(type)
+    func = f"distance:{metric}:{type.value_type}:{type.list_size}"
+    with _lock:
+        if func in pc.list_functions():
+            return func
+
+        def dist(ctx: pc.UdfContext, x: pa.FixedSizeListArray,
+                 q: pa.FixedSizeListScalar) -> pa.Array:
+            from . import torch as io_torch
+
+            xv = io_torch.from_arrow(x)
+            qv = torch.from_numpy(_target_values(q, type))
+            out = coder.distance(qv, xv, metric)[0]
+            return pa.array(out.numpy(), type=type.value_type)
+
+        pc.register_scalar_function(
+            dist,
+            func,
+            {"summary": "fenix distance (GPU)", "description": "coder.py:38-50 on gfx950"},
+            {"x": type, "q": type},
+            type.value_type,
+        )
+    return func
+
+
 def call(
     root: str,
     coding: str | None,

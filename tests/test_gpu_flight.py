@@ -203,6 +203,20 @@ def test_sharded_over_devices(env, monkeypatch):
     assert np.all(np.abs(full.column("__DISTANCE__").to_numpy() - ref) <= 1e-5 * np.abs(ref).max())
 
 
+def test_registered_distance_udf(env):
+    """pc.call_function("distance:{metric}:{T}:{D}", ...) as in index.py:162."""
+    t = O.fill_normal(1, VECTOR_SIZE, seed=35)[0]
+    for metric in ("l2", "cosine", "dot"):
+        func = index.register_distance(metric, VECTOR)
+        assert func == f"distance:{metric}:float:{VECTOR_SIZE}"
+        assert index.register_distance(metric, VECTOR) == func  # idempotent
+        col = env["source"].column("vector").slice(0, 3_500)  # several chunks
+        got = pc.call_function(func, [col, pa.scalar(t, type=VECTOR)]).to_numpy()
+        ref = O.distances(env["x"][:3_500], t[None], metric)[0]
+        scale = 1.0 if metric == "cosine" else float(np.abs(ref).max())
+        assert np.all(np.abs(got - ref) <= 1e-5 * scale)
+
+
 def test_remove(env):
     flight = env["flight"]
     flight.remove()
