@@ -46,6 +46,14 @@ SYMBOLS = (
     "fx_topk_merge_workspace_bytes",
     "fx_topk_merge",
     "fx_fill_normal",
+    "fx_row_sqnorms",
+    "fx_code_assign_workspace_bytes",
+    "fx_code_assign",
+    "fx_kmeans_step_workspace_bytes",
+    "fx_kmeans_step",
+    "fx_code_probe_workspace_bytes",
+    "fx_code_probe",
+    "fx_code_mask",
 )
 
 _lock = threading.Lock()
@@ -95,6 +103,23 @@ def load() -> ctypes.CDLL:
         L.fx_topk_merge.restype = ci
         L.fx_fill_normal.argtypes = [vp, ci, i64, i64, ctypes.c_uint64, i64, i64, vp]
         L.fx_fill_normal.restype = ci
+        L.fx_row_sqnorms.argtypes = [vp, ci, i64, i64, vp, vp]
+        L.fx_row_sqnorms.restype = ci
+        psz = ctypes.POINTER(sz)
+        L.fx_code_assign_workspace_bytes.argtypes = [i64, i64, i64, i64, psz]
+        L.fx_code_assign_workspace_bytes.restype = ci
+        L.fx_code_assign.argtypes = [vp, ci, i64, i64, vp, i64, i64, ci, vp, sz, vp, vp, vp, vp]
+        L.fx_code_assign.restype = ci
+        L.fx_kmeans_step_workspace_bytes.argtypes = [i64, i64, i64, i64, psz]
+        L.fx_kmeans_step_workspace_bytes.restype = ci
+        L.fx_kmeans_step.argtypes = [vp, ci, i64, i64, i64, vp, i64, ci, vp, sz, vp]
+        L.fx_kmeans_step.restype = ci
+        L.fx_code_probe_workspace_bytes.argtypes = [i64, i64, i64, psz]
+        L.fx_code_probe_workspace_bytes.restype = ci
+        L.fx_code_probe.argtypes = [vp, i64, i64, i64, i64, vp, sz, vp, vp, vp, vp]
+        L.fx_code_probe.restype = ci
+        L.fx_code_mask.argtypes = [vp, i64, vp, i64, vp, vp, vp, vp]
+        L.fx_code_mask.restype = ci
         _lib = L
         return L
 
@@ -130,3 +155,21 @@ def device_count() -> int:
     c = ctypes.c_int(0)
     check(load().fx_device_count(ctypes.byref(c)))
     return int(c.value)
+
+
+def _ws(fn, *args) -> int:
+    out = ctypes.c_size_t(0)
+    check(fn(*args, ctypes.byref(out)))
+    return int(out.value)
+
+
+def code_assign_workspace_bytes(n: int, d: int, nb: int, ks: int) -> int:
+    return _ws(load().fx_code_assign_workspace_bytes, n, d, nb, ks)
+
+
+def kmeans_workspace_bytes(nb: int, bs: int, d: int, ks: int) -> int:
+    return _ws(load().fx_kmeans_step_workspace_bytes, nb, bs, d, ks)
+
+
+def code_probe_workspace_bytes(nq: int, nb: int, ks: int) -> int:
+    return _ws(load().fx_code_probe_workspace_bytes, nq, nb, ks)

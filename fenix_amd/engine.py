@@ -343,6 +343,83 @@ class Engine:
             )
         return out
 
+    # ------------------------------------------------------------ coded index
+    def row_sqnorms(self, x: torch.Tensor) -> torch.Tensor:
+        """fx_row_sqnorms: [n] f32 sum of squares of each row of x [n, D]."""
+        out = torch.empty(x.shape[0], dtype=torch.float32, device=self.device)
+        dt = _lib.DTYPE_F32 if x.dtype == torch.float32 else _lib.DTYPE_F16
+        with self.lock:
+            _lib.check(_lib.load().fx_row_sqnorms(_ptr(x), dt, x.shape[0], x.shape[1], _ptr(out),
+                                                  self._stream()))
+        return out
+
+    def code_assign(self, x: torch.Tensor, codewords: torch.Tensor, metric: int,
+                    index: bool = False, code: bool = True, dist: bool = False
+                    ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor],
+                               Optional[torch.Tensor]]:
+        """fx_code_assign: nearest codeword of every row of x [n, D] (f32/f16, on
+        this device) in every codebook of codewords [nb, ks, D] (f32).  Returns
+        (index [n, nb] int32, code [n] int64, dist [n, nb] f32), each or None."""
+        nb, ks, d = codewords.shape
+        n = x.shape[0]
+        cw = codewords.to(self.device, torch.float32).contiguous()
+        dt = _lib.DTYPE_F32 if x.dtype == torch.float32 else _lib.DTYPE_F16
+        oi = torch.empty((n, nb), dtype=torch.int32, device=self.device) if index else None
+        oc = torch.empty(n, dtype=torch.int64, device=self.device) if code else None
+        od = torch.empty((n, nb), dtype=torch.float32, device=self.device) if dist else None
+        with self.lock:
+            ws = self._workspace(_lib.code_assign_workspace_bytes(n, d, nb, ks))
+            _lib.check(_lib.load().fx_code_assign(
+                _ptr(x), dt, n, d, _ptr(cw), nb, ks, metric, _ptr(ws), ws.numel(), _ptr(oi),
+                _ptr(oc), _ptr(od), self._stream()))
+        return oi, oc, od
+
+    def kmeans_step(self, sample: torch.Tensor, codewords: torch.Tensor, metric: int) -> None:
+        """fx_kmeans_step: sample [nb, bs, D] (f32/f16), codewords [nb, ks, D] f32
+        contiguous on this device, updated in place (coder.py:53-65 under vmap)."""
+        nb, bs, d = sample.shape
+        ks = codewords.shape[1]
+        if not (codewords.is_contiguous() and codewords.dtype == torch.float32
+                and codewords.device == self.device):
+            raise ValueError("codewords must be a contiguous float32 tensor on the device")
+        dt = _lib.DTYPE_F32 if sample.dtype == torch.float32 else _lib.DTYPE_F16
+        with self.lock:
+            ws = self._workspace(_lib.kmeans_workspace_bytes(nb, bs, d, ks))
+            _lib.check(_lib.load().fx_kmeans_step(
+                _ptr(sample), dt, nb, bs, d, _ptr(codewords), ks, metric, _ptr(ws), ws.numel(),
+                self._stream()))
+
+    def code_probe(self, cw_dist: torch.Tensor, probes: int, sel: bool = True
+                   ) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
+        """fx_code_probe: cw_dist [nq, nb, ks] f32 -> (codes [nq, probes] int64,
+        scores [nq, probes] f32, selected-code bitmap [nq, words] int32 or None)."""
+        nq, nb, ks = cw_dist.shape
+        cd = cw_dist.to(self.device, torch.float32).contiguous()
+        codes = torch.empty((nq, probes), dtype=torch.int64, device=self.device)
+        scores = torch.empty((nq, probes), dtype=torch.float32, device=self.device)
+        bits = None
+        if sel:
+            words = (ks**nb + 31) // 32
+            bits = torch.empty((nq, words), dtype=torch.int32, device=self.device)
+        with self.lock:
+            ws = self._workspace(_lib.code_probe_workspace_bytes(nq, nb, ks))
+            _lib.check(_lib.load().fx_code_probe(
+                _ptr(cd), nq, nb, ks, probes, _ptr(ws), ws.numel(), _ptr(codes), _ptr(scores),
+                _ptr(bits), self._stream()))
+        return codes, scores, bits
+
+    def code_mask(self, row_code: torch.Tensor, sel: torch.Tensor, ncodes: int,
+                  filter: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """fx_code_mask: (bitmap [ceil(n/32)] int32, kept-row count [1] int64)."""
+        n = row_code.shape[0]
+        out = torch.empty(max(1, (n + 31) // 32), dtype=torch.int32, device=self.device)
+        cnt = torch.empty(1, dtype=torch.int64, device=self.device)
+        with self.lock:
+            _lib.check(_lib.load().fx_code_mask(
+                _ptr(row_code), n, _ptr(sel), ncodes, _ptr(filter), _ptr(out), _ptr(cnt),
+                self._stream()))
+        return out, cnt
+
     def fill(self, out: torch.Tensor, seed: int, row_base: int = 0, cluster: int = 0) -> None:
         """Synthetic corpus (bit-identical to oracle.fill_normal) written in place."""
         dt = _lib.DTYPE_F32 if out.dtype == torch.float32 else _lib.DTYPE_F16

@@ -13,11 +13,13 @@ Mirrors src/fenix/flight.py of the reference:
 
 The wire format (descriptor dict, ``target`` column, result schema) is
 unchanged, so a reference client can talk to this server and vice versa.
-``io.index.call`` underneath runs on the GPU (fenix_amd.io.index).  The coded
-index actions (``make-coder``/``make-index``/``drop-index``, :82-101) are
-outside the MI355X hot path and raise ``NotImplementedError`` server-side,
-which Flight reports to the client as ``FlightServerError`` like any handler
-exception of the reference.
+``io.index.call`` underneath runs on the GPU (fenix_amd.io.index), as do the
+coded-index actions (``make-coder``, ``make-index``, ``drop-index``,
+:82-101: k-means training, table encoding and probe search, io.coder /
+io.index).  ``drop-index`` removes the coding and every index file built
+with it; the reference's loop (:88-93) takes the basename of each index path
+and then splits it on "/", so it never removes an index whose name contains
+"/" and raises ValueError for one that does not.
 """
 
 from __future__ import annotations
@@ -74,9 +76,9 @@ class Server(fl.FlightServerBase):
         source = ticket.ticket.decode().split(":")
 
         if hasattr(self, "coding") and hasattr(self, "column"):
-            raise NotImplementedError("coded-index reads are outside fenix_amd")
-
-        data = io.table.load(self.root, source)
+            data = io.index.load(self.root, self.coding, source, self.column)
+        else:
+            data = io.table.load(self.root, source)
 
         if hasattr(self, "filter"):
             data = data.filter(self.filter)
@@ -107,8 +109,19 @@ class Server(fl.FlightServerBase):
         config = pickle.loads(action.body.to_pybytes())
 
         match action.type:
-            case "make-coder" | "make-index" | "drop-index":
-                raise NotImplementedError("coded-index actions are outside fenix_amd")
+            case "make-coder":
+                io.coder.make(self.root, **config)
+
+            case "make-index":
+                io.index.make(self.root, **config)
+
+            case "drop-index":
+                io.coder.drop(self.root, **config)
+
+                suffix = "/" + config["name"]
+                for path in io.index.list(self.root):
+                    if path.endswith(suffix):
+                        os.unlink(os.path.join(self.root, io.index.LOCATION, path + ".arrow"))
 
             case "drop-table":
                 io.table.drop(self.root, **config)
@@ -203,6 +216,35 @@ class Flight:
 
     def drop_table(self, name: str) -> Self:
         self.conn.do_action(fl.Action("drop-table", pickle.dumps({"name": name})))
+
+        return self
+
+    def make_index(
+        self, name: str, source: str | Sequence[str], column: str, config: dict
+    ) -> Self:
+        self.conn.do_action(
+            fl.Action(
+                "make-coder",
+                pickle.dumps({"name": name, "source": source, "column": column, "config": config}),
+            )
+        )
+
+        return self.sync_index(name, source, column)
+
+    def sync_index(self, name: str, source: str | Sequence[str], column: str) -> Self:
+        self.conn.do_action(
+            fl.Action(
+                "make-index",
+                pickle.dumps({"name": name, "source": source, "column": column}),
+            )
+        )
+
+        return self
+
+    def drop_index(self, name: str) -> Self:
+        self.conn.do_action(
+            fl.Action("drop-index", pickle.dumps({"name": name})),
+        )
 
         return self
 

@@ -1,7 +1,7 @@
 """``fenix_amd.io`` — same module layout as the reference's ``fenix.io``
-(src/fenix/io/__init__.py:1): arrow, table, torch, coder, index.  The coded
-(product-quantised) index and the random batch loader are outside the MI355X
-hot path and are not provided.
+(src/fenix/io/__init__.py:1): arrow, table, torch, coder, index (brute-force
+search and the coded multi-codebook index).  The random batch loader
+(io/batch) is not part of the search path and is not provided.
 
 Submodules load on first use (PEP 562), so a process that only uses the
 Flight client never imports torch or the HIP library: an ``import torch`` in a

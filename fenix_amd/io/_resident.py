@@ -1,0 +1,115 @@
+"""What the search path keeps resident between calls, shared by io.index and io.coder.
+
+* mmap'd Arrow tables, one per file version (io.arrow.load, arrow.py:6-8, is
+  re-run by the reference on every search; here it is re-run only when the
+  file's (size, mtime) changes — do_put rewrites invalidate it);
+* single-chunk copies of small result columns for ``take`` (index.py:166);
+* the HBM shards of embedding columns (engine.CACHE) and of index code
+  columns (``__CODED_ID__``, int64 per row) used to build probe masks on the
+  device.
+"""
+
+from __future__ import annotations
+
+import os
+import threading
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+import pyarrow as pa
+import torch
+
+from .. import engine as _engine
+from . import arrow, table
+
+_lock = threading.Lock()
+_TABLES: Dict[str, Tuple[tuple, pa.Table]] = {}  # path -> (stat key, mmap'd table)
+_COMBINED: Dict[tuple, pa.Array] = {}  # (version, column) -> single-chunk column
+_CODES: Dict[tuple, torch.Tensor] = {}  # (stat key, column, device) -> int64 [rows]
+
+
+def stat_key(path: str) -> tuple:
+    st = os.stat(path)
+    return (os.path.abspath(path), st.st_size, st.st_mtime_ns)
+
+
+def load_table(path: str) -> Tuple[tuple, pa.Table]:
+    """io.arrow.load once per file version."""
+    key = stat_key(path)
+    with _lock:
+        hit = _TABLES.get(key[0])
+        if hit is not None and hit[0] == key:
+            return hit
+    t = arrow.load(path)
+    with _lock:
+        _TABLES[key[0]] = (key, t)
+        for k in [k for k in _COMBINED if key[0] in (s[0] for s in k[0]) and key not in k[0]]:
+            del _COMBINED[k]
+        for k in [k for k in _CODES if k[0][0] == key[0] and k[0] != key]:
+            del _CODES[k]
+    return key, t
+
+
+def sources(root: str, source) -> Tuple[pa.Table, List[Tuple[str, pa.Table]], tuple]:
+    """-> (row-wise joined table, [(path, table)] per source, version key)."""
+    names = [source] if isinstance(source, str) else list(source)
+    loaded = [(table.path(root, n),) + load_table(table.path(root, n)) for n in names]
+    parts = [(p, t) for p, _, t in loaded]
+    return table.join(*[t for _, t in parts]), parts, tuple(k for _, k, _ in loaded)
+
+
+def combined(version: tuple, name: str, col: pa.ChunkedArray) -> pa.Array:
+    key = (version, name)
+    with _lock:
+        comb = _COMBINED.get(key)
+    if comb is None:
+        comb = col.combine_chunks()
+        with _lock:
+            _COMBINED[key] = comb
+    return comb
+
+
+def shards(parts, column: str, devs) -> List[Tuple[_engine.Shard, int, int]]:
+    """HBM shards of every source's ``column``, row-range split over ``devs``.
+    Returns (shard, source index, first source row); global rows continue
+    across sources in order (table.py:19-21)."""
+    out, base = [], 0
+    for i, (path, t) in enumerate(parts):
+        if path is not None:
+            pieces = _engine.CACHE.get(path, t, column, devs).pieces
+        else:
+            pieces = _engine.stage_sharded(t.column(column), devs)
+        out.extend((_engine.Shard(p.data, base + p.start), i, p.start)
+                   for p in pieces if p.data.shape[0])
+        base += t.num_rows
+    return out
+
+
+def gather_rows(shard_list: Sequence[_engine.Shard], rows: np.ndarray,
+                device: torch.device) -> torch.Tensor:
+    """Rows (global, ascending) of the resident shards, in order, on ``device``."""
+    rows = np.asarray(rows, dtype=np.int64)
+    out = []
+    for s in shard_list:
+        lo, hi = np.searchsorted(rows, [s.row_base, s.row_base + s.n])
+        if hi > lo:
+            idx = torch.from_numpy(rows[lo:hi] - s.row_base).to(s.data.device)
+            out.append(s.data.index_select(0, idx).to(device))
+    if not out:
+        raise ValueError("no rows selected")
+    return torch.cat(out) if len(out) > 1 else out[0]
+
+
+def code_column(key: tuple, t: pa.Table, column: str, device: torch.device) -> torch.Tensor:
+    """int64 code column of an index file, resident on ``device`` (cached per file version)."""
+    ck = (key, column, str(device))
+    with _lock:
+        hit = _CODES.get(ck)
+    if hit is not None:
+        return hit
+    col = t.column(column).cast(pa.int64()).fill_null(-1)  # a null code matches no probe
+    host = col.to_numpy() if len(col) else np.zeros(0, np.int64)
+    dev = torch.from_numpy(np.ascontiguousarray(host, dtype=np.int64)).to(device)
+    with _lock:
+        _CODES[ck] = dev
+    return dev

@@ -1,9 +1,11 @@
-"""``call`` — the brute-force search entry point, on the GPU.
+"""``call`` — the search entry point — and the coded index, on the GPU.
 
-Drop-in for ``call`` of src/fenix/io/index/index.py:81-170 (the function
-``Server.do_exchange`` invokes, flight.py:74), brute-force branch
-(``coding=None``, ``probes=None``).  Same signature, argument meaning, output
-schema and error behaviour:
+Drop-in for src/fenix/io/index/index.py of the reference.
+
+``call(root, coding, source, column, target, metric, select, filter, maxval,
+probes)`` (index.py:81-170, the function ``Server.do_exchange`` invokes,
+flight.py:74).  Same signature, argument meaning, output schema and error
+behaviour:
 
 * source: name or list of names under ``<root>/sources`` (index.py:93-97); a
   ``pa.Table`` is also accepted (the reference leaves ``data`` unbound there,
@@ -12,6 +14,13 @@ schema and error behaviour:
   normalised and cast to the column's value type exactly as index.py:101-111
   (``pa.scalar(target, type=column type)``: a wrong length raises
   ``ArrowInvalid``);
+* ``coding`` given: the table is joined with its ``__CODED_ID__`` column
+  (``load``, index.py:19-34); with ``probes`` the metric defaults to the
+  coding's and only rows whose code is among the ``probes`` composites
+  nearest the target are searched (index.py:113-126) — the probe set is
+  computed on the GPU (fx_code_probe) and turned into a row bitmap there
+  (fx_code_mask, AND the filter), which the masked scan consumes without
+  loading the excluded rows;
 * ``select`` default = every column, then ``__DISTANCE__`` appended
   (index.py:128-129); ``assert metric is not None`` (index.py:131); an unknown
   metric raises ``ValueError()`` (coder.py:50);
@@ -23,21 +32,23 @@ schema and error behaviour:
 * the result is one chunk (``combine_chunks``, index.py:170); ``__DISTANCE__``
   has the column's value type (the UDF's output type, index.py:153-159).
 
+``make`` / ``load`` / ``list`` / ``drop`` (index.py:19-78): index files
+``<root>/indexes/<source>/<column>/<name>.arrow`` holding one int64
+``__CODED_ID__`` per row, written in the source's batch layout; ``make``
+encodes the HBM-resident column with fx_code_assign (MFMA nearest codeword per
+codebook) instead of the per-batch pyarrow UDF (index.py:46-49).
+
 What changes underneath: the corpus column is resident in HBM (engine.CACHE)
 instead of re-read and scanned per chunk by a Python UDF, top-k is fused into
 the gfx950 scan, and only the k winning rows are gathered (chunk-aware, no
 ``Table.take`` over the whole chunked vector column, index.py:166).
-The coded (product-quantised) index — ``load``/``make``/``list``/``drop`` of
-index.py:19-78 and the ``coding``/``probes`` branch (index.py:95, 113-126) — is
-approximate search outside the MI355X hot path and raises
-``NotImplementedError``.
 """
 
 from __future__ import annotations
 
 import os
 import threading
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Iterator, List, Sequence
 
 import numpy as np
 import pyarrow as pa
@@ -46,43 +57,11 @@ import torch
 from torch import Tensor
 
 from .. import engine as _engine
-from . import arrow, coder, table
+from . import _resident, arrow, coder, table
 
 CODE_COL: str = "__CODED_ID__"
 DIST_COL: str = "__DISTANCE__"
 LOCATION: str = "indexes"
-
-
-_lock = threading.Lock()
-_TABLES: Dict[str, Tuple[tuple, pa.Table]] = {}  # path -> (stat key, mmap'd table)
-_COMBINED: Dict[tuple, pa.Array] = {}  # (stat keys, column) -> single-chunk column
-
-
-def _load(path: str) -> Tuple[tuple, pa.Table]:
-    """io.arrow.load (arrow.py:6-8) once per file version: the mmap'd table is
-    reused while (size, mtime) are unchanged; do_put rewrites invalidate it."""
-    st = os.stat(path)
-    key = (os.path.abspath(path), st.st_size, st.st_mtime_ns)
-    with _lock:
-        hit = _TABLES.get(key[0])
-        if hit is not None and hit[0] == key:
-            return hit
-    t = arrow.load(path)
-    with _lock:
-        _TABLES[key[0]] = (key, t)
-        for k in [k for k in _COMBINED if key[0] in (s[0] for s in k[0]) and key not in k[0]]:
-            del _COMBINED[k]
-    return key, t
-
-
-def _sources(root: str, source):
-    """-> (joined table, [(path or None, table)], version key or None)."""
-    if isinstance(source, pa.Table):
-        return source, [(None, source)], None
-    names = [source] if isinstance(source, str) else list(source)
-    loaded = [(table.path(root, n),) + _load(table.path(root, n)) for n in names]
-    parts = [(p, t) for p, _, t in loaded]
-    return table.join(*[t for _, t in parts]), parts, tuple(k for _, k, _ in loaded)
 
 
 def _target_values(target, type: pa.DataType) -> np.ndarray:
@@ -159,33 +138,14 @@ def _take_columns(data: pa.Table, cols: List[str], rows: np.ndarray, column: str
         col = data.column(c)
         if c == column and col.null_count == 0:
             arrays.append(_gather_vectors(shards, rows, col.type))
-            continue
-        if version is None:
+        elif version is None:
             arrays.append(_take_chunked(col, rows))
-            continue
-        key = (version, c)
-        with _lock:
-            comb = _COMBINED.get(key)
-        if comb is None:
-            comb = col.combine_chunks()
-            with _lock:
-                _COMBINED[key] = comb
-        arrays.append(comb.take(pa.array(rows)))
+        else:
+            arrays.append(_resident.combined(version, c, col).take(pa.array(rows)))
     return pa.Table.from_arrays(arrays, schema=data.select(cols).schema)
 
 
-def _shards(parts, column: str, devs):
-    """HBM shards of every source, row-range split over ``devs``; global rows
-    continue across sources in order (table.py:19-21)."""
-    shards, base = [], 0
-    for path, t in parts:
-        if path is not None:
-            pieces = _engine.CACHE.get(path, t, column, devs).pieces
-        else:
-            pieces = _engine.stage_sharded(t.column(column), devs)
-        shards.extend(_engine.Shard(p.data, base + p.start) for p in pieces if p.data.shape[0])
-        base += t.num_rows
-    return shards
+_register_lock = threading.Lock()
 
 
 def register_distance(metric: str, type: pa.DataType) -> str:
@@ -201,7 +161,7 @@ def register_distance(metric: str, type: pa.DataType) -> str:
     coder.metric_id(metric)
     _engine.value_dtype(type)
     func = f"distance:{metric}:{type.value_type}:{type.list_size}"
-    with _lock:
+    with _register_lock:
         if func in pc.list_functions():
             return func
 
@@ -224,6 +184,131 @@ def register_distance(metric: str, type: pa.DataType) -> str:
     return func
 
 
+def _index_path(root: str, name: str, source: str, column: str) -> str:
+    return os.path.join(root, LOCATION, source, column, name + ".arrow")
+
+
+def load(root: str, name: str, source: str | Sequence[str], column: str) -> pa.Table:
+    """index.py:19-34: the source table(s) with their ``__CODED_ID__`` column."""
+    if isinstance(source, str):
+        coder.load(root, name)
+
+        path = _index_path(root, name, source, column)
+
+        return table.join(table.load(root, source), arrow.load(path), axis=1)
+
+    assert isinstance(source, Sequence) and not isinstance(source, str)
+    return table.join(*[load(root, name, s, column) for s in source])
+
+
+def _encode(root: str, source: str, column: str, code: coder.Coding) -> tuple:
+    """Composite code of every row of one source: fx_code_assign over its HBM
+    shards.  -> (source table, int64 codes)."""
+    _, t = _resident.load_table(table.path(root, source))
+    parts = [(table.path(root, source), t)]
+    out = np.zeros(t.num_rows, dtype=np.int64)
+    m = coder.metric_id(code["config"]["metric"])
+    for s, _, start in _resident.shards(parts, column, _engine.devices()):
+        dev = s.data.device
+        with torch.cuda.device(dev):
+            _, c, _ = _engine.Engine.get(dev).code_assign(s.data, code["tensor"], m)
+            out[start : start + s.n] = c.cpu().numpy()
+    return t, out
+
+
+def make(root: str, name: str, source: str | Sequence[str], column: str) -> pa.Table:
+    """index.py:37-65: encode the source(s) with the coding ``name`` and write
+    the code column, one record batch per source batch."""
+    if isinstance(source, str):
+        path = _index_path(root, name, source, column)
+
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+
+        code = coder.load(root, name)
+        t, codes = _encode(root, source, column, code)
+
+        def record_batch_generator():
+            start = 0
+            for batch in t.to_batches():
+                n = batch.num_rows
+                yield pa.record_batch([pa.array(codes[start : start + n])], names=[CODE_COL])
+                start += n
+
+        arrow.make(
+            path,
+            pa.RecordBatchReader.from_batches(
+                pa.schema({CODE_COL: pa.int64()}),
+                record_batch_generator(),
+            ),
+        )
+
+        return load(root, name, source, column)
+
+    assert isinstance(source, Sequence) and not isinstance(source, str)
+    return table.join(*[make(root, name, s, column) for s in source])
+
+
+def list(root: str) -> Iterator[str]:
+    """index.py:68-71: index files as ``<source>/<column>/<name>``."""
+    base = os.path.join(root, LOCATION)
+    for dirpath, _, files in os.walk(base):
+        for f in sorted(files):
+            if f.endswith(".arrow"):
+                rel = os.path.relpath(os.path.join(dirpath, f), base)
+                yield rel.removesuffix(".arrow")
+
+
+def drop(root: str, name: str, source: str, column: str) -> None:
+    path = _index_path(root, name, source, column)
+
+    if os.path.exists(path):
+        os.unlink(path)
+
+
+def _unpack(words: torch.Tensor, n: int) -> np.ndarray:
+    w = words.cpu().numpy().view(np.uint8)
+    return np.unpackbits(w, bitorder="little")[:n].astype(bool)
+
+
+def _probe_masks(code: coder.Coding, q: np.ndarray, probes: int, shard_info, code_parts,
+                 masks):
+    """index.py:113-126 on the device: the ``probes`` composites nearest the
+    target (with the coding's metric, as pc.call_function(coding, ...) does),
+    then per shard bit r = code[r] in that set AND the filter bit.
+    -> (per-shard masks, kept-row count, lazy host mask)."""
+    nb = int(code["config"]["num_codebooks"])
+    ks = int(code["config"]["codebook_size"])
+    total = ks**nb
+    if probes > total:
+        raise RuntimeError("selected index k out of range")  # torch.topk in coder.call
+    dev0 = shard_info[0][0].data.device if shard_info else _engine.devices()[0]
+    with torch.cuda.device(dev0):
+        eng0 = _engine.Engine.get(dev0)
+        cw = code["tensor"].to(dev0, torch.float32).contiguous()
+        qd = torch.from_numpy(q).to(dev0)
+        d = eng0.distances(_engine.Shard(cw.reshape(nb * ks, -1), 0), qd,
+                           coder.metric_id(code["config"]["metric"]))
+        _, _, sel = eng0.code_probe(d.reshape(1, nb, ks), int(probes), sel=True)
+    out, counts = [], []
+    for i, (s, src, start) in enumerate(shard_info):
+        dev = s.data.device
+        with torch.cuda.device(dev):
+            key, t = code_parts[src]
+            rc = _resident.code_column(key, t, CODE_COL, dev)[start : start + s.n]
+            mk, cnt = _engine.Engine.get(dev).code_mask(
+                rc, sel[0].to(dev), total, masks[i] if masks is not None else None)
+        out.append(mk)
+        counts.append(cnt)
+    n_rows = int(sum(int(c.item()) for c in counts))
+
+    def host() -> np.ndarray:
+        if not out:
+            return np.zeros(0, dtype=bool)
+        return np.concatenate([_unpack(mk, s.n) for mk, (s, _, _) in zip(out, shard_info)])
+
+    return out, n_rows, host
+
+
 def call(
     root: str,
     coding: str | None,
@@ -236,14 +321,29 @@ def call(
     maxval: int | None = None,
     probes: int | None = None,
 ) -> pa.Table:
-    if coding is not None or probes is not None:
-        raise NotImplementedError(
-            "coded-index (product-quantised) search is outside the fenix_amd brute-force path"
-        )
+    code_parts = None
+    if isinstance(source, pa.Table):
+        data, parts, version = source, [(None, source)], None
+    else:
+        names = [source] if isinstance(source, str) else [*source]
+        data, parts, version = _resident.sources(root, names)
+        if coding is not None:
+            coder.load(root, coding)
+            code_parts = [_resident.load_table(_index_path(root, coding, s, column))
+                          for s in names]
+            data = table.join(*[table.join(t, it, axis=1)
+                                for (_, t), (_, it) in zip(parts, code_parts)])
+            version = version + tuple(k for k, _ in code_parts)
 
-    data, parts, version = _sources(root, source)
     type = data.schema.field(column).type
     q = _target_values(target, type)
+
+    code = None
+    if coding is not None and probes is not None:
+        code = coder.load(root, coding)
+
+        if metric is None:
+            metric = code["config"]["metric"]
 
     select = [*select] if select is not None else data.column_names
     select = select + [DIST_COL]
@@ -253,14 +353,21 @@ def call(
     m = coder.metric_id(metric)
     _engine.value_dtype(type)
 
-    mask = _filter_mask(data, filter) if filter is not None else None
-    n_rows = int(mask.sum()) if mask is not None else data.num_rows
-
-    shards = _shards(parts, column, _engine.devices())
+    fmask = _filter_mask(data, filter) if filter is not None else None
+    shard_info = _resident.shards(parts, column, _engine.devices())
+    shards = [s for s, _, _ in shard_info]
     masks = None
-    if mask is not None:
-        masks = [_engine.device_mask(mask[s.row_base : s.row_base + s.n], s.data.device)
+    if fmask is not None:
+        masks = [_engine.device_mask(fmask[s.row_base : s.row_base + s.n], s.data.device)
                  for s in shards]
+    if code is not None:
+        if code_parts is None:
+            raise ValueError("a probe search needs named sources with an index")
+        masks, n_rows, host_mask = _probe_masks(code, q, probes, shard_info, code_parts, masks)
+    else:
+        n_rows = int(fmask.sum()) if fmask is not None else data.num_rows
+        host_mask = (lambda: fmask) if fmask is not None else None
+
     qt = torch.from_numpy(q)
     base_cols = [c for c in dict.fromkeys(select) if c != DIST_COL]
 
@@ -274,8 +381,9 @@ def call(
     else:
         dist = _engine.distances_all(shards, qt, m, masks)[0]
         out = data.select(base_cols)
-        if mask is not None:
-            out = out.filter(pa.array(mask))
-            dist = dist[mask]
+        if host_mask is not None:
+            hm = host_mask()
+            out = out.filter(pa.array(hm))
+            dist = dist[hm]
     out = out.append_column(DIST_COL, pa.array(dist.astype(type.value_type.to_pandas_dtype())))
     return out.select(select).combine_chunks()

@@ -144,6 +144,76 @@ int fx_topk_merge(const float* in_dist, const int64_t* in_row, int64_t nq, int64
 int fx_fill_normal(void* x, int dtype, int64_t n, int64_t d, uint64_t seed, int64_t row_base,
                    int64_t cluster, void* stream);
 
+/*
+ * Per-row sum of squares in f32: out[r] = sum_c x[r][c]^2 (x: [n][d] f32/f16).
+ * The ||x||^2 term of the L2 expansion and the cosine norms (F.normalize,
+ * coder.py:43-44, 55-56).
+ */
+int fx_row_sqnorms(const void* x, int dtype, int64_t n, int64_t d, float* out, void* stream);
+
+/* ---------------------------------------------------------------- coded index
+ * A coding (src/fenix/io/coder/coder.py:24-35) is nb = num_codebooks
+ * independent codebooks of ks = codebook_size full-width f32 codewords,
+ * codewords[nb][ks][d].  The composite code of a row is
+ *     sum_j argmin_c dist(x, codewords[j][c]) * ks^(nb-1-j)
+ * (coder.py:171-186 with maxval = 1, as index.make encodes a table,
+ * index.py:37-65).  Ties go to the lowest codeword index.
+ */
+
+/*
+ * Nearest codeword of every row in every codebook.  x: [n][d] corpus rows
+ * (f32/f16).  Outputs (each nullable): out_index [n][nb] int32 codeword index,
+ * out_code [n] int64 composite code (needs ks^nb < 2^31), out_dist [n][nb] f32
+ * the metric's distance to the chosen codeword.  Replaces the per-batch
+ * pc.call_function(coding, [x, 1]) of index.py:46-49 -> coder.call
+ * (coder.py:143-194) and the argmin of coder.update (coder.py:58-59).
+ */
+int fx_code_assign_workspace_bytes(int64_t n, int64_t d, int64_t nb, int64_t ks,
+                                   size_t* out_bytes);
+int fx_code_assign(const void* x, int dtype, int64_t n, int64_t d, const float* codewords,
+                   int64_t nb, int64_t ks, int metric, void* ws, size_t ws_bytes,
+                   int32_t* out_index, int64_t* out_code, float* out_dist, void* stream);
+
+/*
+ * One mini-batch k-means step of every codebook, in place: the body of the
+ * training loop, coding = vmap(update)(coding, sample) (coder.py:53-65, 118).
+ * sample: [nb][bs][d] rows (f32/f16), slice j trains codebook j;
+ * codewords: [nb][ks][d] f32, updated in place.  cosine: codewords and sample
+ * rows are normalised first and the result is normalised again; every
+ * codeword becomes the mean of itself and the rows assigned to it
+ * (torch.index_reduce "mean", include_self), summed in row order.
+ */
+int fx_kmeans_step_workspace_bytes(int64_t nb, int64_t bs, int64_t d, int64_t ks,
+                                   size_t* out_bytes);
+int fx_kmeans_step(const void* sample, int dtype, int64_t nb, int64_t bs, int64_t d,
+                   float* codewords, int64_t ks, int metric, void* ws, size_t ws_bytes,
+                   void* stream);
+
+/*
+ * Probe selection (coder.py:171-186, index.py:113-121): cw_dist [nq][nb][ks]
+ * holds each target's distance to every codeword (fx_knn_distances with the
+ * codewords as the corpus); the composite score of code c is the sum over
+ * j = 0..nb-1 (in that order, f32) of the distance to its digit j.  Emits the
+ * `probes` best composites per target in (score, code) order: out_code
+ * [nq][probes] int64, out_score [nq][probes] f32, out_sel [nq][ceil(ks^nb/32)]
+ * bitmap of the selected codes (each nullable).  ks^nb * nq < 2^31.
+ */
+int fx_code_probe_workspace_bytes(int64_t nq, int64_t nb, int64_t ks, size_t* out_bytes);
+int fx_code_probe(const float* cw_dist, int64_t nq, int64_t nb, int64_t ks, int64_t probes,
+                  void* ws, size_t ws_bytes, int64_t* out_code, float* out_score,
+                  uint32_t* out_sel, void* stream);
+
+/*
+ * Row bitmap of a probe search: bit r = (row_code[r] is set in sel) AND
+ * (filter == NULL or bit r of filter).  The filter expression
+ * pc.field("__CODED_ID__").isin(probe codes) & filter of index.py:117-126,
+ * consumed as the `mask` of fx_knn_search.  out_mask: ceil(n/32) words;
+ * out_count (nullable, one uint64 on the device): the number of rows kept —
+ * len(data) after the filter, which decides maxval's branch (index.py:165).
+ */
+int fx_code_mask(const int64_t* row_code, int64_t n, const uint32_t* sel, int64_t ncodes,
+                 const uint32_t* filter, uint32_t* out_mask, uint64_t* out_count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -121,7 +121,7 @@ def test_call_argument_errors(tmp_path):
         index.call(root, None, "s", "vector", target=q, metric=None, maxval=5)
     with pytest.raises(ValueError):  # coder.py:50
         index.call(root, None, "s", "vector", target=q, metric="hamming", maxval=5)
-    with pytest.raises(NotImplementedError):  # coded index is out of scope
+    with pytest.raises(FileNotFoundError):  # coder.load of a missing coding (coder.py:73)
         index.call(root, "code", "s", "vector", target=q, metric="l2", maxval=5, probes=4)
     with pytest.raises(pa.ArrowInvalid):  # index.py:111 length check
         index.call(root, None, "s", "vector", target=q[:-1], metric="l2", maxval=5)
@@ -161,3 +161,49 @@ def test_flight_table_admin_without_gpu(tmp_path):
         assert not os.path.exists(tmp_path / "root")
     finally:
         server.shutdown()
+
+
+def test_coding_file_roundtrip_and_udf(tmp_path):
+    """coder.load (coder.py:68-91) without a GPU: the file format loads with
+    weights_only=True, the UDF ``name`` is registered with the reference's
+    signature, list/drop work; a file holding a pickled pa.DataType (what the
+    reference writes) is refused instead of unpickled."""
+    import torch
+
+    from fenix_amd.io import coder
+
+    root = str(tmp_path)
+    name = "cpu/l2"
+    vt = pa.list_(pa.float32(), 8)
+    os.makedirs(os.path.join(root, coder.LOCATION, "cpu"))
+    cfg = {"metric": "l2", "codebook_size": 4, "num_codebooks": 2, "batch_size": 16,
+           "num_epochs": 1}
+    t = torch.arange(64, dtype=torch.float32).reshape(2, 4, 8)
+    with open(coder._path(root, name), "wb") as f:
+        torch.save({"tensor": t, "column": coder._type_bytes(vt), "config": cfg}, f)
+    c = coder.load(root, name)
+    assert c["column"] == vt and c["config"] == cfg
+    assert torch.equal(c["tensor"], t)
+    assert name in pc.list_functions()
+    fn = pc.get_function(name)
+    assert fn.arity == 2
+    assert list(coder.list(root)) == [name]
+    with open(coder._path(root, "cpu/bad"), "wb") as f:
+        torch.save({"tensor": t, "column": vt, "config": cfg}, f)
+    with pytest.raises(ValueError):
+        coder.load(root, "cpu/bad")
+    coder.drop(root, name)
+    assert list(coder.list(root)) == ["cpu/bad"]
+
+
+def test_index_files_list_and_drop(tmp_path):
+    root = str(tmp_path)
+    for src, col, name in [("a/b", "vector", "c/l2"), ("t", "v", "dot")]:
+        p = index._index_path(root, name, src, col)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        fenix_amd.io.arrow.make(p, pa.RecordBatchReader.from_batches(
+            pa.schema({index.CODE_COL: pa.int64()}),
+            [pa.record_batch([pa.array([1, 2], pa.int64())], names=[index.CODE_COL])]))
+    assert sorted(index.list(root)) == ["a/b/vector/c/l2", "t/v/dot"]
+    index.drop(root, "dot", "t", "v")
+    assert list(index.list(root)) == ["a/b/vector/c/l2"]
