@@ -54,6 +54,10 @@ SYMBOLS = (
     "fx_code_probe_workspace_bytes",
     "fx_code_probe",
     "fx_code_mask",
+    "fx_knn_search_rows_workspace_bytes",
+    "fx_knn_search_rows",
+    "fx_mask_compact_workspace_bytes",
+    "fx_mask_compact",
 )
 
 _lock = threading.Lock()
@@ -120,6 +124,15 @@ def load() -> ctypes.CDLL:
         L.fx_code_probe.restype = ci
         L.fx_code_mask.argtypes = [vp, i64, vp, i64, vp, vp, vp, vp]
         L.fx_code_mask.restype = ci
+        L.fx_knn_search_rows_workspace_bytes.argtypes = [i64, i64, ci, i64, i64, psz]
+        L.fx_knn_search_rows_workspace_bytes.restype = ci
+        L.fx_knn_search_rows.argtypes = [vp, ci, i64, i64, i64, vp, i64, vp, i64, ci, i64, vp, sz,
+                                         vp, vp, vp]
+        L.fx_knn_search_rows.restype = ci
+        L.fx_mask_compact_workspace_bytes.argtypes = [i64, psz]
+        L.fx_mask_compact_workspace_bytes.restype = ci
+        L.fx_mask_compact.argtypes = [vp, i64, vp, sz, vp, vp, vp]
+        L.fx_mask_compact.restype = ci
         _lib = L
         return L
 
@@ -173,3 +186,11 @@ def kmeans_workspace_bytes(nb: int, bs: int, d: int, ks: int) -> int:
 
 def code_probe_workspace_bytes(nq: int, nb: int, ks: int) -> int:
     return _ws(load().fx_code_probe_workspace_bytes, nq, nb, ks)
+
+
+def search_rows_workspace_bytes(nrows: int, d: int, dtype: int, nq: int, k: int) -> int:
+    return _ws(load().fx_knn_search_rows_workspace_bytes, nrows, d, dtype, nq, k)
+
+
+def compact_workspace_bytes(n: int) -> int:
+    return _ws(load().fx_mask_compact_workspace_bytes, n)

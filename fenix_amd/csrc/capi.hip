@@ -470,6 +470,75 @@ int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
                        out_dist, out_row, stream);
 }
 
+int fx_knn_search_rows_workspace_bytes(int64_t nrows, int64_t d, int dtype, int64_t nq,
+                                       int64_t k, size_t* out_bytes) {
+  if (!out_bytes) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  int rc = validate(nrows, d, dtype, nq, FX_METRIC_L2);
+  if (rc) return rc;
+  if (k < 1 || k > kMaxK) {
+    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kMaxK);
+    return FX_EUNSUPPORTED;
+  }
+  SearchLayout s;
+  rc = plan_single(nrows, d, dtype, nq, k, FX_METRIC_L2, true, &s);
+  if (rc) return rc;
+  *out_bytes = s.total;
+  return FX_OK;
+}
+
+int fx_knn_search_rows(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                       const int32_t* rows, int64_t nrows, const float* queries, int64_t nq,
+                       int metric, int64_t k, void* ws, size_t ws_bytes, float* out_dist,
+                       int64_t* out_row, void* stream) {
+  int rc = validate(nrows, d, dtype, nq, metric);
+  if (rc) return rc;
+  if (k < 1 || k > kMaxK) {
+    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kMaxK);
+    return FX_EUNSUPPORTED;
+  }
+  if (!corpus || !ws || !queries || !out_dist || !out_row || (nrows > 0 && !rows)) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  if (row_base < 0 || n < 0 || row_base + n >= 0xffffffffll || n > 0x7fffffffll) {
+    set_error("global rows [%lld, %lld) exceed the 32-bit row space", (long long)row_base,
+              (long long)(row_base + n));
+    return FX_EUNSUPPORTED;
+  }
+  SearchLayout s;
+  rc = plan_single(nrows, d, dtype, nq, k, metric, ((uintptr_t)corpus % 16) == 0, &s);
+  if (rc) return rc;
+  if (ws_bytes < s.total) {
+    set_error("workspace too small: %zu < %zu", ws_bytes, s.total);
+    return FX_EINVAL;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  uint64_t* lists = reinterpret_cast<uint64_t*>(ws);
+  ScanArgs a = {};
+  a.X = corpus;
+  a.n = nrows;
+  a.d = (int)d;
+  a.row_base = row_base;
+  a.rows = rows;
+  a.rows_per_block = s.scan.rows_per_block;
+  a.k = (int)k;
+  a.cap = s.scan.cap;
+  a.qbytes = s.scan.qbytes;
+  a.mode = kModeTopk;
+  for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
+    const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
+    a.q = queries + (size_t)q0 * d;
+    a.out_lists = lists + (size_t)q0 * s.scan.nlists * k;
+    rc = launch_scan(s.scan, a, qn, st);
+    if (rc) return rc;
+  }
+  return run_merge(s.merge, lists, nq, k, reinterpret_cast<char*>(ws) + s.lists_bytes, out_dist,
+                   out_row, st);
+}
+
 int fx_knn_distances(const void* corpus, int dtype, int64_t n, int64_t d,
                      const float* queries, int64_t nq, int metric, const uint32_t* mask,
                      float* out, void* stream) {

@@ -16,6 +16,7 @@ struct ScanArgs {
   int64_t row_base;       // global row of local row 0
   const float* q;         // [nq][d]
   const uint32_t* mask;   // bitmap or null
+  const int32_t* rows;    // [n] corpus rows to scan (n = list length) or null: rows 0..n-1
   int64_t rows_per_block;
   int k;
   int cap;                // per-wave candidate list capacity

@@ -335,27 +335,39 @@ __global__ void normalize_kernel(float* __restrict__ X, int64_t n, int d) {
 }
 
 // k-means codeword update (coder.py:59-63): block (c, j) averages codeword c of
-// codebook j with the sample rows assigned to it, in row order.
+// codebook j with the sample rows assigned to it.  1024 threads; thread t owns
+// dims t, t+1024, ... in registers (d <= 16384); each 1024-entry slice of the
+// assignments is compacted in LDS (ballot, row order) and its rows are summed
+// four at a time (independent loads in flight).  The order of the sum is fixed:
+// deterministic, no float atomics.
+constexpr int kUpdThreads = 1024;
+constexpr int kUpdDims = 16;  // registers per thread: d <= 16 * 1024
+
 template <typename T>
-__global__ void __launch_bounds__(256) update_kernel(const T* __restrict__ X, int64_t bs, int d,
-                                                     const int32_t* __restrict__ assign,
-                                                     const float* __restrict__ rnorm,
-                                                     float* __restrict__ W, int ks, int cosine) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* acc = reinterpret_cast<float*>(smem);
-  __shared__ int list[256];
-  __shared__ int wcount[4];
-  __shared__ float red[4];
+__global__ void __launch_bounds__(kUpdThreads) update_kernel(const T* __restrict__ X, int64_t bs,
+                                                             int d,
+                                                             const int32_t* __restrict__ assign,
+                                                             const float* __restrict__ rnorm,
+                                                             float* __restrict__ W, int ks,
+                                                             int cosine) {
+  __shared__ int list[kUpdThreads];
+  __shared__ int wcount[16];
+  __shared__ float red[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int c = blockIdx.x, j = blockIdx.y;
   float* w = W + ((int64_t)j * ks + c) * d;
   const T* Xj = X + (int64_t)j * bs * d;
   const int32_t* as = assign + (int64_t)j * bs;
   const float* rn = rnorm ? rnorm + (int64_t)j * bs : nullptr;
-  for (int i = tid; i < d; i += 256) acc[i] = w[i];  // include_self
+  float acc[kUpdDims];
+#pragma unroll
+  for (int u = 0; u < kUpdDims; ++u) {
+    const int dim = tid + u * kUpdThreads;
+    acc[u] = dim < d ? w[dim] : 0.f;  // include_self
+  }
   int count = 1;
   const uint64_t ltmask = (1ull << lane) - 1ull;
-  for (int64_t i0 = 0; i0 < bs; i0 += 256) {
+  for (int64_t i0 = 0; i0 < bs; i0 += kUpdThreads) {
     const int64_t i = i0 + tid;
     const bool m = i < bs && as[i] == c;
     const uint64_t b = __ballot(m);
@@ -363,61 +375,62 @@ __global__ void __launch_bounds__(256) update_kernel(const T* __restrict__ X, in
     __syncthreads();
     int base = 0, total = 0;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < 16; ++v) {
       base += v < wid ? wcount[v] : 0;
       total += wcount[v];
     }
     if (m) list[base + __popcll(b & ltmask)] = (int)(i - i0);
     __syncthreads();
-    for (int e = 0; e < total; ++e) {
-      const int64_t r = i0 + list[e];
-      const T* xr = Xj + r * d;
-      if (cosine) {
-        const float nrm = rn[r];
-        for (int dim = tid; dim < d; dim += 256) acc[dim] += (float)xr[dim] / nrm;
-      } else {
-        for (int dim = tid; dim < d; dim += 256) acc[dim] += (float)xr[dim];
+    for (int e0 = 0; e0 < total; e0 += 4) {
+      const T* xr[4];
+      float sc[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int e = e0 + t < total ? e0 + t : e0;
+        const int64_t r = i0 + list[e];
+        xr[t] = Xj + r * d;
+        sc[t] = (e0 + t < total) ? 1.f : 0.f;
+        if (cosine && e0 + t < total) sc[t] = rn[r];
+      }
+#pragma unroll
+      for (int u = 0; u < kUpdDims; ++u) {
+        const int dim = tid + u * kUpdThreads;
+        if (dim < d) {
+          float v[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] = (float)xr[t][dim];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (e0 + t < total) acc[u] += cosine ? v[t] / sc[t] : v[t];
+          }
+        }
       }
     }
     count += total;
     __syncthreads();
   }
   float sq = 0.f;
-  for (int dim = tid; dim < d; dim += 256) {
-    const float v = acc[dim] / (float)count;
-    acc[dim] = v;
-    sq = fmaf(v, v, sq);
+#pragma unroll
+  for (int u = 0; u < kUpdDims; ++u) {
+    acc[u] = acc[u] / (float)count;
+    if (tid + u * kUpdThreads < d) sq = fmaf(acc[u], acc[u], sq);
   }
+  float nrm = 1.f;
   if (cosine) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) sq += __shfl_xor(sq, m);
     if (lane == 0) red[wid] = sq;
     __syncthreads();
-    const float nrm = fmaxf(sqrtf(red[0] + red[1] + red[2] + red[3]), 1e-12f);
-    for (int dim = tid; dim < d; dim += 256) w[dim] = acc[dim] / nrm;
-  } else {
-    for (int dim = tid; dim < d; dim += 256) w[dim] = acc[dim];
+    float t = 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) t += red[v];
+    nrm = fmaxf(sqrtf(t), 1e-12f);
   }
-}
-
-// composite scores (coder.py:171-181): sum over codebooks j = 0..nb-1, in that
-// order, of the target's distance to codeword digit_j(c) of codebook j, where
-// c = sum_j digit_j * ks^(nb-1-j).
-__global__ void composite_kernel(const float* __restrict__ dist, int nb, int ks, int64_t C,
-                                 uint64_t* __restrict__ keys) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t q = blockIdx.y;
-  if (c >= C) return;
-  int digit[32];
-  int64_t rem = c;
-  for (int j = nb - 1; j >= 0; --j) {
-    digit[j] = (int)(rem % ks);
-    rem /= ks;
+#pragma unroll
+  for (int u = 0; u < kUpdDims; ++u) {
+    const int dim = tid + u * kUpdThreads;
+    if (dim < d) w[dim] = cosine ? acc[u] / nrm : acc[u];
   }
-  const float* dq = dist + q * (int64_t)nb * ks;
-  float s = 0.f;
-  for (int j = 0; j < nb; ++j) s = s + dq[j * ks + digit[j]];
-  keys[q * C + c] = make_comp(s, (uint32_t)c);
 }
 
 __global__ void offsets_kernel(int* off, int64_t nq, int64_t C) {
@@ -438,23 +451,141 @@ __global__ void emit_kernel(const uint64_t* __restrict__ sorted, int64_t C, int6
   if (sel) atomicOr(&sel[q * words + (code >> 5)], 1u << (code & 31));
 }
 
-__global__ void mask_kernel(const int64_t* __restrict__ code, int64_t n,
-                            const uint32_t* __restrict__ sel, int64_t ncodes,
-                            const uint32_t* __restrict__ filter, uint32_t* __restrict__ out,
-                            int64_t words, unsigned long long* __restrict__ count) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  bool bit = false;
-  if (row < n) {
-    const int64_t c = code[row];
-    bit = c >= 0 && c < ncodes && ((sel[c >> 5] >> (c & 31)) & 1u);
-    if (filter != nullptr) bit = bit && ((filter[row >> 5] >> (row & 31)) & 1u);
+// grid-stride over rows; one count atomic per block (a per-wave atomic on one
+// address serialised the kernel: 340 us for 10M rows)
+__global__ void __launch_bounds__(256) mask_kernel(const int64_t* __restrict__ code, int64_t n,
+                                                   const uint32_t* __restrict__ sel, int64_t ncodes,
+                                                   const uint32_t* __restrict__ filter,
+                                                   uint32_t* __restrict__ out, int64_t words,
+                                                   unsigned long long* __restrict__ count) {
+  __shared__ unsigned int wsum[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned int kept = 0;
+  for (int64_t base = (int64_t)blockIdx.x * 256; base < n; base += (int64_t)gridDim.x * 256) {
+    const int64_t row = base + threadIdx.x;
+    bool bit = false;
+    if (row < n) {
+      const int64_t c = code[row];
+      bit = c >= 0 && c < ncodes && ((sel[c >> 5] >> (c & 31)) & 1u);
+      if (filter != nullptr) bit = bit && ((filter[row >> 5] >> (row & 31)) & 1u);
+    }
+    const uint64_t b = __ballot(bit);
+    const int64_t w0 = (row - lane) >> 5;
+    if (lane == 0 && w0 < words) out[w0] = (uint32_t)b;
+    if (lane == 32 && w0 + 1 < words) out[w0 + 1] = (uint32_t)(b >> 32);
+    kept += (unsigned int)__popcll(b);
   }
-  const uint64_t b = __ballot(bit);
-  const int64_t w0 = (row - lane) >> 5;
-  if (lane == 0 && w0 < words) out[w0] = (uint32_t)b;
-  if (lane == 32 && w0 + 1 < words) out[w0 + 1] = (uint32_t)(b >> 32);
-  if (count != nullptr && lane == 0 && b != 0ull) atomicAdd(count, (unsigned long long)__popcll(b));
+  if (count == nullptr) return;
+  if (lane == 0) wsum[wid] = kept;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (t) atomicAdd(count, (unsigned long long)t);
+  }
+}
+
+// ---- ordered bitmap -> row list compaction (three passes, no atomics)
+constexpr int kCompactWords = 2048;  // words (65 536 rows) per block
+
+__global__ void __launch_bounds__(256) compact_count_kernel(const uint32_t* __restrict__ mask,
+                                                            int64_t words,
+                                                            uint32_t* __restrict__ block_count) {
+  __shared__ unsigned int wsum[4];
+  const int64_t w0 = (int64_t)blockIdx.x * kCompactWords;
+  unsigned int c = 0;
+  for (int i = threadIdx.x; i < kCompactWords; i += 256)
+    if (w0 + i < words) c += __popc(mask[w0 + i]);
+  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) block_count[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// one 1024-thread block: exclusive scan of the block counts (in place), total
+__global__ void __launch_bounds__(1024) compact_scan_kernel(uint32_t* __restrict__ v, int64_t nb,
+                                                            unsigned long long* __restrict__ total) {
+  __shared__ unsigned int wsum[16];
+  __shared__ unsigned int carry;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < nb; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const unsigned int x = i < nb ? v[i] : 0u;
+    const unsigned int incl = wave_incl_scan(x, lane);
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    unsigned int before = carry;
+    for (int w = 0; w < wid; ++w) before += wsum[w];
+    if (i < nb) v[i] = before + incl - x;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = before + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && total != nullptr) *total = carry;
+}
+
+// each thread owns 8 consecutive words; block scan of thread sums gives offsets
+__global__ void __launch_bounds__(256) compact_write_kernel(const uint32_t* __restrict__ mask,
+                                                            int64_t words,
+                                                            const uint32_t* __restrict__ offs,
+                                                            int32_t* __restrict__ rows) {
+  __shared__ unsigned int wsum[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t w0 = (int64_t)blockIdx.x * kCompactWords + threadIdx.x * 8;
+  uint32_t m[8];
+  unsigned int c = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = (w0 + j < words) ? mask[w0 + j] : 0u;
+    c += __popc(m[j]);
+  }
+  const unsigned int incl = wave_incl_scan(c, lane);
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  unsigned int pos = offs[blockIdx.x] + incl - c;
+  for (int w = 0; w < wid; ++w) pos += wsum[w];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t bits = m[j];
+    while (bits) {
+      const int b = __ffs(bits) - 1;
+      rows[pos++] = (int32_t)((w0 + j) * 32 + b);
+      bits &= bits - 1;
+    }
+  }
+}
+
+// probe codes from the merged (score, code) lists -> selected-code bitmap
+__global__ void sel_kernel(const int64_t* __restrict__ codes, int64_t p, uint32_t* __restrict__ sel,
+                           int64_t words) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t q = blockIdx.y;
+  if (i >= p) return;
+  const int64_t c = codes[q * p + i];
+  if (c >= 0) atomicOr(&sel[q * words + (c >> 5)], 1u << (c & 31));
+}
+
+// composite keys as [nq][nlists][kin] lists for the merge kernels (kEmpty pad)
+__global__ void composite_lists_kernel(const float* __restrict__ dist, int nb, int ks, int64_t C,
+                                       int64_t padded, uint64_t* __restrict__ keys) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t q = blockIdx.y;
+  if (c >= padded) return;
+  if (c >= C) {
+    keys[q * padded + c] = kEmpty;
+    return;
+  }
+  int digit[32];
+  int64_t rem = c;
+  for (int j = nb - 1; j >= 0; --j) {
+    digit[j] = (int)(rem % ks);
+    rem /= ks;
+  }
+  const float* dq = dist + q * (int64_t)nb * ks;
+  float s = 0.f;
+  for (int j = 0; j < nb; ++j) s = s + dq[j * ks + digit[j]];
+  keys[q * padded + c] = make_comp(s, (uint32_t)c);
 }
 
 size_t align256(size_t v) { return (v + 255) / 256 * 256; }
@@ -585,11 +716,17 @@ int64_t composite_count(int64_t nb, int64_t ks) {
   return c < ((int64_t)1 << 31) ? c : -1;
 }
 
+constexpr int64_t kProbeMerge = 4096;  // probes up to this go through the merge kernels
+
 struct ProbeLayout {
-  int64_t C;
-  size_t temp_bytes, off_keys, off_sorted, off_off, off_temp, total;
+  int64_t C, kin, nlists, padded, pmax;
+  size_t temp_bytes, merge_bytes;
+  size_t off_keys, off_sorted, off_off, off_temp, off_merge, off_codes, off_scores, total;
 };
 
+// composite scores of coder.call (coder.py:171-181): probes <= 4096 are
+// selected by the merge kernels (keys viewed as lists of kin), larger probe
+// sets (and the full argsort of maxval=None) by a segmented radix sort.
 int probe_layout(int64_t nq, int64_t nb, int64_t ks, ProbeLayout* p) {
   p->C = composite_count(nb, ks);
   if (p->C < 0 || nq * p->C >= ((int64_t)1 << 31) || nb > 32) {
@@ -597,6 +734,14 @@ int probe_layout(int64_t nq, int64_t nb, int64_t ks, ProbeLayout* p) {
               (long long)nb, (long long)nq);
     return FX_EUNSUPPORTED;
   }
+  p->kin = p->C < kProbeMerge ? p->C : kProbeMerge;
+  p->nlists = (p->C + p->kin - 1) / p->kin;
+  p->padded = p->nlists * p->kin;
+  p->pmax = p->C < kProbeMerge ? p->C : kProbeMerge;
+  MergePlan mp;
+  int rc = plan_merge(nq, p->nlists, p->kin, p->pmax, &mp);
+  if (rc) return rc;
+  p->merge_bytes = mp.ws_bytes;
   p->temp_bytes = 0;
   hipError_t e = hipcub::DeviceSegmentedRadixSort::SortKeys(
       nullptr, p->temp_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)(nq * p->C),
@@ -607,13 +752,19 @@ int probe_layout(int64_t nq, int64_t nb, int64_t ks, ProbeLayout* p) {
   }
   size_t off = 0;
   p->off_keys = off;
-  off += align256((size_t)nq * p->C * 8);
+  off += align256((size_t)nq * p->padded * 8);
   p->off_sorted = off;
   off += align256((size_t)nq * p->C * 8);
   p->off_off = off;
   off += align256((size_t)(nq + 1) * 4);
   p->off_temp = off;
   off += align256(p->temp_bytes);
+  p->off_merge = off;
+  off += align256(p->merge_bytes);
+  p->off_codes = off;
+  off += align256((size_t)nq * p->pmax * 8);
+  p->off_scores = off;
+  off += align256((size_t)nq * p->pmax * 4);
   p->total = off;
   return FX_OK;
 }
@@ -701,8 +852,8 @@ int fx_kmeans_step(const void* sample, int dtype, int64_t nb, int64_t bs, int64_
     set_error("fx_kmeans_step: invalid arguments");
     return FX_EINVAL;
   }
-  if (d * 4 > 64 * 1024) {
-    set_error("fx_kmeans_step: d=%lld exceeds the LDS accumulator (16384)", (long long)d);
+  if (d > kUpdDims * kUpdThreads) {
+    set_error("fx_kmeans_step: d=%lld exceeds %d", (long long)d, kUpdDims * kUpdThreads);
     return FX_EUNSUPPORTED;
   }
   const AssignLayout l = assign_layout(nb, bs, 1, ks, d);
@@ -739,21 +890,15 @@ int fx_kmeans_step(const void* sample, int dtype, int64_t nb, int64_t bs, int64_
                      (int)ks, metric, assign, (int64_t*)nullptr, (float*)nullptr);
   rc = check_launch("finalize_kernel");
   if (rc) return rc;
-  const size_t smem = (size_t)d * 4;
   const dim3 grid((unsigned)ks, (unsigned)nb);
-  if (dtype == FX_DTYPE_F32) {
-    (void)hipFuncSetAttribute((const void*)update_kernel<float>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-    hipLaunchKernelGGL(update_kernel<float>, grid, dim3(256), smem, stream,
+  if (dtype == FX_DTYPE_F32)
+    hipLaunchKernelGGL(update_kernel<float>, grid, dim3(kUpdThreads), 0, stream,
                        reinterpret_cast<const float*>(sample), bs, (int)d, assign,
                        cosine ? rnorm : nullptr, codewords, (int)ks, cosine ? 1 : 0);
-  } else {
-    (void)hipFuncSetAttribute((const void*)update_kernel<_Float16>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-    hipLaunchKernelGGL(update_kernel<_Float16>, grid, dim3(256), smem, stream,
+  else
+    hipLaunchKernelGGL(update_kernel<_Float16>, grid, dim3(kUpdThreads), 0, stream,
                        reinterpret_cast<const _Float16*>(sample), bs, (int)d, assign,
                        cosine ? rnorm : nullptr, codewords, (int)ks, cosine ? 1 : 0);
-  }
   return check_launch("update_kernel");
 }
 
@@ -791,30 +936,54 @@ int fx_code_probe(const float* cw_dist, int64_t nq, int64_t nb, int64_t ks, int6
   }
   char* w = reinterpret_cast<char*>(ws);
   uint64_t* keys = reinterpret_cast<uint64_t*>(w + p.off_keys);
-  uint64_t* sorted = reinterpret_cast<uint64_t*>(w + p.off_sorted);
-  int* off = reinterpret_cast<int*>(w + p.off_off);
-  hipLaunchKernelGGL(composite_kernel, dim3((unsigned)((p.C + 255) / 256), (unsigned)nq),
-                     dim3(256), 0, stream, cw_dist, (int)nb, (int)ks, p.C, keys);
-  rc = check_launch("composite_kernel");
-  if (rc) return rc;
-  hipLaunchKernelGGL(offsets_kernel, dim3((unsigned)((nq + 256) / 256)), dim3(256), 0, stream, off,
-                     nq, p.C);
-  rc = check_launch("offsets_kernel");
-  if (rc) return rc;
-  size_t temp = p.temp_bytes;
-  hipError_t e = hipcub::DeviceSegmentedRadixSort::SortKeys(
-      w + p.off_temp, temp, keys, sorted, (int)(nq * p.C), (int)nq, off, off + 1, 0, 64, stream);
-  if (e != hipSuccess) {
-    set_error("segmented sort: %s", hipGetErrorString(e));
-    return FX_EHIP;
-  }
   const int64_t words = (p.C + 31) / 32;
+  hipError_t e;
   if (out_sel != nullptr) {
     e = hipMemsetAsync(out_sel, 0, (size_t)nq * words * 4, stream);
     if (e != hipSuccess) {
       set_error("probe memset: %s", hipGetErrorString(e));
       return FX_EHIP;
     }
+  }
+  if (probes <= kProbeMerge) {
+    hipLaunchKernelGGL(composite_lists_kernel,
+                       dim3((unsigned)((p.padded + 255) / 256), (unsigned)nq), dim3(256), 0,
+                       stream, cw_dist, (int)nb, (int)ks, p.C, p.padded, keys);
+    rc = check_launch("composite_lists_kernel");
+    if (rc) return rc;
+    MergePlan mp;
+    rc = plan_merge(nq, p.nlists, p.kin, probes, &mp);
+    if (rc) return rc;
+    if (mp.ws_bytes > p.merge_bytes) {
+      set_error("probe merge workspace %zu > %zu", mp.ws_bytes, p.merge_bytes);
+      return FX_EUNSUPPORTED;
+    }
+    int64_t* codes = out_code ? out_code : reinterpret_cast<int64_t*>(w + p.off_codes);
+    float* scores = out_score ? out_score : reinterpret_cast<float*>(w + p.off_scores);
+    rc = run_merge(mp, keys, nq, probes, w + p.off_merge, scores, codes, stream);
+    if (rc) return rc;
+    if (out_sel == nullptr) return FX_OK;
+    hipLaunchKernelGGL(sel_kernel, dim3((unsigned)((probes + 255) / 256), (unsigned)nq),
+                       dim3(256), 0, stream, codes, probes, out_sel, words);
+    return check_launch("sel_kernel");
+  }
+  uint64_t* sorted = reinterpret_cast<uint64_t*>(w + p.off_sorted);
+  int* off = reinterpret_cast<int*>(w + p.off_off);
+  hipLaunchKernelGGL(composite_lists_kernel, dim3((unsigned)((p.C + 255) / 256), (unsigned)nq),
+                     dim3(256), 0, stream, cw_dist, (int)nb, (int)ks, p.C, p.C, keys);
+  rc = check_launch("composite_lists_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(offsets_kernel, dim3((unsigned)((nq + 256) / 256)), dim3(256), 0, stream, off,
+                     nq, p.C);
+  rc = check_launch("offsets_kernel");
+  if (rc) return rc;
+  size_t temp = p.temp_bytes;
+  e = hipcub::DeviceSegmentedRadixSort::SortKeys(w + p.off_temp, temp, keys, sorted,
+                                                 (int)(nq * p.C), (int)nq, off, off + 1, 0, 64,
+                                                 stream);
+  if (e != hipSuccess) {
+    set_error("segmented sort: %s", hipGetErrorString(e));
+    return FX_EHIP;
   }
   hipLaunchKernelGGL(emit_kernel, dim3((unsigned)((probes + 255) / 256), (unsigned)nq), dim3(256),
                      0, stream, sorted, p.C, probes, out_code, out_score, out_sel, words);
@@ -839,10 +1008,67 @@ int fx_code_mask(const int64_t* row_code, int64_t n, const uint32_t* sel, int64_
   }
   if (n == 0) return FX_OK;
   const int64_t words = (n + 31) / 32;
-  hipLaunchKernelGGL(mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+  int cus = 0;
+  int rc = device_cus(&cus);
+  if (rc) return rc;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > (int64_t)cus * 8) blocks = (int64_t)cus * 8;
+  hipLaunchKernelGGL(mask_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
                      row_code, n, sel, ncodes, filter, out_mask, words,
                      reinterpret_cast<unsigned long long*>(out_count));
   return check_launch("mask_kernel");
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int fx_mask_compact_workspace_bytes(int64_t n, size_t* out_bytes) {
+  if (out_bytes == nullptr || n < 0) {
+    set_error("fx_mask_compact_workspace_bytes: invalid arguments");
+    return FX_EINVAL;
+  }
+  const int64_t words = (n + 31) / 32;
+  const int64_t blocks = (words + kCompactWords - 1) / kCompactWords;
+  *out_bytes = align256((size_t)(blocks > 0 ? blocks : 1) * 4);
+  return FX_OK;
+}
+
+int fx_mask_compact(const uint32_t* mask, int64_t n, void* ws, size_t ws_bytes, int32_t* out_rows,
+                    uint64_t* out_count, void* stream_) {
+  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+  if (n < 0 || n > 0x7fffffffll || (n > 0 && (mask == nullptr || out_rows == nullptr ||
+                                               ws == nullptr))) {
+    set_error("fx_mask_compact: invalid arguments");
+    return FX_EINVAL;
+  }
+  const int64_t words = (n + 31) / 32;
+  const int64_t blocks = (words + kCompactWords - 1) / kCompactWords;
+  if (ws_bytes < (size_t)blocks * 4) {
+    set_error("workspace too small: %zu < %zu", ws_bytes, (size_t)blocks * 4);
+    return FX_EINVAL;
+  }
+  if (n == 0) {
+    if (out_count == nullptr) return FX_OK;
+    hipError_t e = hipMemsetAsync(out_count, 0, 8, stream);
+    if (e != hipSuccess) {
+      set_error("compact memset: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+    return FX_OK;
+  }
+  uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
+  hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, mask,
+                     words, counts);
+  int rc = check_launch("compact_count_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, stream, counts, blocks,
+                     reinterpret_cast<unsigned long long*>(out_count));
+  rc = check_launch("compact_scan_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(compact_write_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, mask,
+                     words, counts, out_rows);
+  return check_launch("compact_write_kernel");
 }
 
 }  // extern "C"

@@ -195,7 +195,8 @@ __device__ int wave_compact(uint64_t* buf, int cnt, uint64_t T, int quota_eq, in
 template <typename T, int W, int L, int U>
 struct RowTile {
   typename VecT<T, W>::type v[U][L];
-  int64_t row[U];
+  int64_t row[U];  // position in the scanned range (list index with a row list)
+  int64_t src[U];  // corpus row (== row without a row list)
   bool valid[U];
 };
 
@@ -220,12 +221,14 @@ __device__ __forceinline__ void tile_load(RowTile<T, W, L, U>& t, int64_t it, in
   for (int u = 0; u < U; ++u) {
     t.row[u] = it + u * 4 + c.grp;
     t.valid[u] = t.row[u] < c.hi;
+    t.src[u] = t.row[u];
+    if (a.rows != nullptr && t.valid[u]) t.src[u] = a.rows[t.row[u]];
     if (a.mask != nullptr && t.valid[u])
-      t.valid[u] = (a.mask[t.row[u] >> 5] >> (t.row[u] & 31)) & 1u;
+      t.valid[u] = (a.mask[t.src[u] >> 5] >> (t.src[u] & 31)) & 1u;
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const V* rp = reinterpret_cast<const V*>(X + t.row[u] * (int64_t)a.d);
+    const V* rp = reinterpret_cast<const V*>(X + t.src[u] * (int64_t)a.d);
 #pragma unroll
     for (int cc = 0; cc < L; ++cc) {
       const int s = ch * 16 * L + cc * 16 + c.jl;
@@ -298,7 +301,7 @@ __device__ __forceinline__ void tile_finish(const RowTile<T, W, L, U>& t, float 
   const uint64_t ltmask = (1ull << c.lane) - 1ull;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const uint64_t comp = make_comp(dist[u], (uint32_t)(a.row_base + t.row[u]));
+    const uint64_t comp = make_comp(dist[u], (uint32_t)(a.row_base + t.src[u]));
     const bool p = (c.jl == 0) && t.valid[u] && comp < thr;
     const uint64_t b = __ballot(p);
     if (b) {

@@ -307,25 +307,64 @@ class Engine:
         )
         return od, orow
 
+    def compact(self, mask: torch.Tensor, n: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """fx_mask_compact: (ascending int32 rows [n capacity], count [1] int64); caller holds lock."""
+        rows = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        cnt = torch.empty(1, dtype=torch.int64, device=self.device)
+        ws = self._workspace(_lib.compact_workspace_bytes(n))
+        _lib.check(_lib.load().fx_mask_compact(_ptr(mask), n, _ptr(ws), ws.numel(), _ptr(rows),
+                                               _ptr(cnt), self._stream()))
+        return rows, cnt
+
+    def search_rows(self, shard: Shard, rows: torch.Tensor, nrows: int, queries: torch.Tensor,
+                    metric: int, k: int, out_dist: torch.Tensor, out_row: torch.Tensor) -> None:
+        """fx_knn_search_rows over the listed local rows; caller holds lock."""
+        nq = queries.shape[0]
+        ws = self._workspace(_lib.search_rows_workspace_bytes(nrows, shard.d, shard.dtype_id, nq, k))
+        _lib.check(_lib.load().fx_knn_search_rows(
+            _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base, _ptr(rows), nrows,
+            _ptr(queries), nq, metric, k, _ptr(ws), ws.numel(), _ptr(out_dist), _ptr(out_row),
+            self._stream()))
+
+    # a mask keeping less than this fraction of a shard is compacted to a row
+    # list, so the scan reads only the kept rows (a masked scan still walks all)
+    SPARSE = 0.5
+
+    def _search_one(self, shard: Shard, queries: torch.Tensor, metric: int, k: int,
+                    mask: Optional[torch.Tensor], count: Optional[int], out_dist: torch.Tensor,
+                    out_row: torch.Tensor) -> None:
+        if mask is not None and count is not None and count < self.SPARSE * shard.n:
+            if count == 0:
+                out_dist.fill_(float("nan"))
+                out_row.fill_(-1)
+                return
+            rows, _ = self.compact(mask, shard.n)
+            self.search_rows(shard, rows, int(count), queries, metric, k, out_dist, out_row)
+            return
+        self.search_shard(shard, queries, metric, k, mask, out_dist, out_row)
+
     def search(self, shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: int,
-               masks: Optional[Sequence[Optional[torch.Tensor]]] = None
+               masks: Optional[Sequence[Optional[torch.Tensor]]] = None,
+               counts: Optional[Sequence[Optional[int]]] = None,
                ) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Exact top-k over several shards (sources): per-shard scan, then merge."""
+        """Exact top-k over several shards (sources): per-shard scan, then merge.
+        ``counts`` (optional): rows each mask keeps, to pick the row-list scan."""
         queries = queries.to(self.device, torch.float32).contiguous()
         nq = queries.shape[0]
+        mask_of = (lambda i: masks[i]) if masks else (lambda i: None)
+        count_of = (lambda i: counts[i]) if counts else (lambda i: None)
         with self.lock:
             if len(shards) == 1:
                 od = torch.empty((nq, k), dtype=torch.float32, device=self.device)
                 orow = torch.empty((nq, k), dtype=torch.int64, device=self.device)
-                self.search_shard(shards[0], queries, metric, k, masks[0] if masks else None,
-                                  od, orow)
+                self._search_one(shards[0], queries, metric, k, mask_of(0), count_of(0), od, orow)
                 return od, orow
             pd = torch.empty((nq, len(shards), k), dtype=torch.float32, device=self.device)
             pr = torch.empty((nq, len(shards), k), dtype=torch.int64, device=self.device)
             for i, sh in enumerate(shards):
                 td = torch.empty((nq, k), dtype=torch.float32, device=self.device)
                 tr = torch.empty((nq, k), dtype=torch.int64, device=self.device)
-                self.search_shard(sh, queries, metric, k, masks[i] if masks else None, td, tr)
+                self._search_one(sh, queries, metric, k, mask_of(i), count_of(i), td, tr)
                 pd[:, i] = td
                 pr[:, i] = tr
             return self.merge(pd, pr, k)
@@ -446,7 +485,8 @@ def device_mask(mask: Optional[np.ndarray], device: torch.device) -> Optional[to
 
 
 def search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: int,
-               masks: Optional[Sequence[Optional[torch.Tensor]]] = None
+               masks: Optional[Sequence[Optional[torch.Tensor]]] = None,
+               counts: Optional[Sequence[Optional[int]]] = None,
                ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Exact top-k over shards that may live on several devices.
 
@@ -464,7 +504,8 @@ def search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: i
         with torch.cuda.device(dev):
             eng = Engine.get(dev)
             ms = [masks[i] for i in idx] if masks is not None else None
-            per.append(eng.search([shards[i] for i in idx], queries, metric, k, ms))
+            cs = [counts[i] for i in idx] if counts is not None else None
+            per.append(eng.search([shards[i] for i in idx], queries, metric, k, ms, cs))
     if len(per) == 1:
         return per[0]
     dev0 = next(iter(groups))

@@ -109,7 +109,7 @@ def code_column(key: tuple, t: pa.Table, column: str, device: torch.device) -> t
         return hit
     col = t.column(column).cast(pa.int64()).fill_null(-1)  # a null code matches no probe
     host = col.to_numpy() if len(col) else np.zeros(0, np.int64)
-    dev = torch.from_numpy(np.ascontiguousarray(host, dtype=np.int64)).to(device)
+    dev = torch.from_numpy(np.array(host, dtype=np.int64)).to(device)  # writable copy
     with _lock:
         _CODES[ck] = dev
     return dev

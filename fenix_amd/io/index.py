@@ -81,7 +81,7 @@ def _target_values(target, type: pa.DataType) -> np.ndarray:
     if target.type != type:
         target = target.cast(type)
     values = target.values.to_numpy(zero_copy_only=False)
-    return np.asarray(values, dtype=np.float32).reshape(1, -1)
+    return np.array(values, dtype=np.float32).reshape(1, -1)  # writable copy
 
 
 def _filter_mask(data: pa.Table, filter: pc.Expression) -> np.ndarray:
@@ -275,7 +275,7 @@ def _probe_masks(code: coder.Coding, q: np.ndarray, probes: int, shard_info, cod
     """index.py:113-126 on the device: the ``probes`` composites nearest the
     target (with the coding's metric, as pc.call_function(coding, ...) does),
     then per shard bit r = code[r] in that set AND the filter bit.
-    -> (per-shard masks, kept-row count, lazy host mask)."""
+    -> (per-shard masks, per-shard kept rows, kept-row total, lazy host mask)."""
     nb = int(code["config"]["num_codebooks"])
     ks = int(code["config"]["codebook_size"])
     total = ks**nb
@@ -299,14 +299,15 @@ def _probe_masks(code: coder.Coding, q: np.ndarray, probes: int, shard_info, cod
                 rc, sel[0].to(dev), total, masks[i] if masks is not None else None)
         out.append(mk)
         counts.append(cnt)
-    n_rows = int(sum(int(c.item()) for c in counts))
+    counts = [int(c.item()) for c in counts]
+    n_rows = sum(counts)
 
     def host() -> np.ndarray:
         if not out:
             return np.zeros(0, dtype=bool)
         return np.concatenate([_unpack(mk, s.n) for mk, (s, _, _) in zip(out, shard_info)])
 
-    return out, n_rows, host
+    return out, counts, n_rows, host
 
 
 def call(
@@ -363,16 +364,19 @@ def call(
     if code is not None:
         if code_parts is None:
             raise ValueError("a probe search needs named sources with an index")
-        masks, n_rows, host_mask = _probe_masks(code, q, probes, shard_info, code_parts, masks)
+        masks, counts, n_rows, host_mask = _probe_masks(code, q, probes, shard_info, code_parts,
+                                                         masks)
     else:
         n_rows = int(fmask.sum()) if fmask is not None else data.num_rows
         host_mask = (lambda: fmask) if fmask is not None else None
+        counts = [int(fmask[s.row_base : s.row_base + s.n].sum()) for s in shards] \
+            if fmask is not None else None
 
     qt = torch.from_numpy(q)
     base_cols = [c for c in dict.fromkeys(select) if c != DIST_COL]
 
     if maxval is not None and n_rows > maxval:
-        dist, rows = _engine.search_all(shards, qt, m, int(maxval), masks)
+        dist, rows = _engine.search_all(shards, qt, m, int(maxval), masks, counts)
         dist = dist[0].cpu().numpy()
         rows = rows[0].cpu().numpy()
         keep = rows >= 0

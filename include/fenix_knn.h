@@ -111,6 +111,21 @@ int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
                   int64_t* out_row, void* stream);
 
 /*
+ * fx_knn_search over a list of corpus rows instead of all of them: rows
+ * [nrows] int32 local row numbers (< n, device), e.g. the rows kept by a
+ * filter or a probe set (fx_mask_compact).  The scan reads only the listed
+ * rows, so a selective filter (index.py:161) or probe set (index.py:113-126)
+ * costs its own bytes, not the corpus's.  Results use global rows
+ * (row_base + listed row) and the same ordering contract; nrows >= 1.
+ */
+int fx_knn_search_rows_workspace_bytes(int64_t nrows, int64_t d, int dtype, int64_t nq,
+                                       int64_t k, size_t* out_bytes);
+int fx_knn_search_rows(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                       const int32_t* rows, int64_t nrows, const float* queries, int64_t nq,
+                       int metric, int64_t k, void* ws, size_t ws_bytes, float* out_dist,
+                       int64_t* out_row, void* stream);
+
+/*
  * All distances of nq queries to every corpus row: out[nq][n] float32.
  * Replaces the per-chunk UDF / coder.distance (index.py:137-151, coder.py:38-50)
  * where the reference returns the whole table (maxval None or n <= maxval,
@@ -213,6 +228,15 @@ int fx_code_probe(const float* cw_dist, int64_t nq, int64_t nb, int64_t ks, int6
  */
 int fx_code_mask(const int64_t* row_code, int64_t n, const uint32_t* sel, int64_t ncodes,
                  const uint32_t* filter, uint32_t* out_mask, uint64_t* out_count, void* stream);
+
+/*
+ * Row bitmap -> ascending list of the set rows (int32), and their count
+ * (out_count: one uint64 on the device, nullable).  Three passes, no atomics,
+ * deterministic.  n < 2^31.
+ */
+int fx_mask_compact_workspace_bytes(int64_t n, size_t* out_bytes);
+int fx_mask_compact(const uint32_t* mask, int64_t n, void* ws, size_t ws_bytes, int32_t* out_rows,
+                    uint64_t* out_count, void* stream);
 
 #ifdef __cplusplus
 }

@@ -365,3 +365,59 @@ def test_batched_equals_unbatched(eng, monkeypatch):
     check_topk(bd, br, od, orow, xh, q, "cosine")
     check_topk(sd, sr, od, orow, xh, q, "cosine")
     assert np.max(np.abs(bd - sd)) <= 1e-6
+
+
+# ---------------------------------------------------------------- row lists
+
+
+@pytest.mark.parametrize("n,frac", [(1, 1.0), (1000, 0.3), (100_003, 0.01), (300_000, 0.45)])
+def test_mask_compact_is_ordered_nonzero(eng, n, frac):
+    rs = np.random.RandomState(n)
+    keep = rs.rand(n) < frac
+    m = device_mask(keep, eng.device)
+    with eng.lock:
+        rows, cnt = eng.compact(m, n)
+    torch.cuda.synchronize()
+    c = int(cnt.item())
+    assert c == int(keep.sum())
+    np.testing.assert_array_equal(rows.cpu().numpy()[:c], np.nonzero(keep)[0])
+
+
+@pytest.mark.parametrize("metric", METRICS)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_row_list_search_equals_masked_search(eng, metric, dtype):
+    """fx_knn_search_rows over the compacted rows == the masked full scan,
+    bit for bit, and == the oracle over the kept rows."""
+    n, d, k = 200_000, 96, 50
+    x = gpu_fill(eng, n, d, seed=61, dtype=dtype, row_base=0, cluster=1000)
+    q = O.fill_normal(2, d, seed=62)
+    keep = np.random.RandomState(5).rand(n) < 0.05
+    qt = torch.from_numpy(q).to(eng.device)
+    m = device_mask(keep, eng.device)
+    mid = _lib.METRICS[metric]
+    d_mask, r_mask = eng.search([Shard(x, 1000)], qt, mid, k, [m])
+    d_rows, r_rows = eng.search([Shard(x, 1000)], qt, mid, k, [m], [int(keep.sum())])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(r_rows.cpu().numpy(), r_mask.cpu().numpy())
+    np.testing.assert_array_equal(d_rows.cpu().numpy(), d_mask.cpu().numpy())
+    xh = O.fill_normal(n, d, 61, cluster=1000,
+                       dtype=np.float32 if dtype == torch.float32 else np.float16)
+    od, orow = O.knn(xh.astype(np.float32), q, metric, k, mask=keep)
+    check_topk(d_rows.cpu().numpy(), r_rows.cpu().numpy() - 1000, od, orow, xh.astype(np.float32),
+               q, metric)
+
+
+def test_row_list_search_empty_and_all(eng):
+    n, d, k = 5000, 32, 10
+    x = gpu_fill(eng, n, d, seed=63)
+    qt = torch.from_numpy(O.fill_normal(1, d, seed=64)).to(eng.device)
+    none = device_mask(np.zeros(n, bool), eng.device)
+    dd, rr = eng.search([Shard(x, 0)], qt, _lib.METRIC_L2, k, [none], [0])
+    torch.cuda.synchronize()
+    assert np.all(rr.cpu().numpy() == -1) and np.all(np.isnan(dd.cpu().numpy()))
+    one = np.zeros(n, bool)
+    one[1234] = True
+    dd, rr = eng.search([Shard(x, 0)], qt, _lib.METRIC_L2, k,
+                        [device_mask(one, eng.device)], [1])
+    torch.cuda.synchronize()
+    assert rr.cpu().numpy()[0, 0] == 1234 and np.all(rr.cpu().numpy()[0, 1:] == -1)

@@ -22,6 +22,9 @@ for step in "$@"; do
   case $step in
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    testcoder) run pytest_coder 900 python -u -m pytest tests/test_gpu_coder.py -m gpu -q -x -p no:cacheprovider ;;
+    coded) run coded 600 python -u tools/bench_coded.py ;;
+    profcoded) run profcoded 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profcoded -o run --output-format csv -- python3 -u tools/bench_coded.py --iters 3 ;;
     testk) run pytest_kernels 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_fullsize.py -m gpu -q -x -p no:cacheprovider ;;
     testsall) run pytest_gpu 1500 python -u -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python -u bench.py ;;
