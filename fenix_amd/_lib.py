@@ -58,6 +58,9 @@ SYMBOLS = (
     "fx_knn_search_rows",
     "fx_mask_compact_workspace_bytes",
     "fx_mask_compact",
+    "fx_comm_init_all",
+    "fx_comm_destroy",
+    "fx_allgather_topk",
 )
 
 _lock = threading.Lock()
@@ -133,6 +136,13 @@ def load() -> ctypes.CDLL:
         L.fx_mask_compact_workspace_bytes.restype = ci
         L.fx_mask_compact.argtypes = [vp, i64, vp, sz, vp, vp, vp]
         L.fx_mask_compact.restype = ci
+        L.fx_comm_init_all.argtypes = [ci, ctypes.POINTER(ci), ctypes.POINTER(vp)]
+        L.fx_comm_init_all.restype = ci
+        L.fx_comm_destroy.argtypes = [vp]
+        L.fx_comm_destroy.restype = ci
+        pvp = ctypes.POINTER(vp)
+        L.fx_allgather_topk.argtypes = [vp, pvp, pvp, i64, i64, pvp, pvp, pvp]
+        L.fx_allgather_topk.restype = ci
         _lib = L
         return L
 

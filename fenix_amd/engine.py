@@ -508,6 +508,9 @@ def search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: i
             per.append(eng.search([shards[i] for i in idx], queries, metric, k, ms, cs))
     if len(per) == 1:
         return per[0]
+    devs = list(groups)
+    if os.environ.get("FENIX_AMD_GATHER", "p2p") == "rccl":
+        return DeviceComm.get(devs).gather_merge(per, k)
     dev0 = next(iter(groups))
     with torch.cuda.device(dev0):
         eng0 = Engine.get(dev0)
@@ -515,6 +518,66 @@ def search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: i
         rr = torch.stack([r.to(dev0) for _, r in per], dim=1)
         with eng0.lock:
             return eng0.merge(dd, rr, k)
+
+
+class DeviceComm:
+    """fx_comm_init_all over distinct devices (one RCCL rank each), cached.
+
+    ``gather_merge`` all-gathers every device's [nq, k] top-k with one grouped
+    fx_allgather_topk and merges on the first device.  ``search_all`` uses it
+    when FENIX_AMD_GATHER=rccl; the default gathers with peer copies (the lists
+    are a few KB, a copy per device is one xGMI hop)."""
+
+    _cache: Dict[tuple, "DeviceComm"] = {}
+    _clock = threading.Lock()
+
+    def __init__(self, devs: Sequence[torch.device]) -> None:
+        self.devs = list(devs)
+        ids = (ctypes.c_int * len(devs))(*[d.index for d in devs])
+        handle = ctypes.c_void_p()
+        _lib.check(_lib.load().fx_comm_init_all(len(devs), ids, ctypes.byref(handle)))
+        self.handle = handle
+
+    @classmethod
+    def get(cls, devs: Sequence[torch.device]) -> "DeviceComm":
+        key = tuple(d.index for d in devs)
+        with cls._clock:
+            c = cls._cache.get(key)
+            if c is None:
+                c = cls(devs)
+                cls._cache[key] = c
+            return c
+
+    def close(self) -> None:
+        if self.handle:
+            _lib.check(_lib.load().fx_comm_destroy(self.handle))
+            self.handle = None
+
+    def allgather(self, per: Sequence[Tuple[torch.Tensor, torch.Tensor]]
+                  ) -> List[Tuple[torch.Tensor, torch.Tensor]]:
+        """per[i] = (dist [nq, k] f32, row [nq, k] i64) on devs[i] ->
+        [(dist [ndev, nq, k], row [ndev, nq, k])] on every device."""
+        n = len(self.devs)
+        nq, k = per[0][0].shape
+        outs = [(torch.empty((n, nq, k), dtype=torch.float32, device=dv),
+                 torch.empty((n, nq, k), dtype=torch.int64, device=dv)) for dv in self.devs]
+        P = ctypes.c_void_p * n
+        src_d = P(*[d.contiguous().data_ptr() for d, _ in per])
+        src_r = P(*[r.contiguous().data_ptr() for _, r in per])
+        dst_d = P(*[d.data_ptr() for d, _ in outs])
+        dst_r = P(*[r.data_ptr() for _, r in outs])
+        streams = P(*[torch.cuda.current_stream(dv).cuda_stream for dv in self.devs])
+        _lib.check(_lib.load().fx_allgather_topk(self.handle, src_d, src_r, nq, k, dst_d, dst_r,
+                                                 streams))
+        return outs
+
+    def gather_merge(self, per, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        d, r = self.allgather(per)[0]
+        dev0 = self.devs[0]
+        with torch.cuda.device(dev0):
+            eng0 = Engine.get(dev0)
+            with eng0.lock:
+                return eng0.merge(d.permute(1, 0, 2), r.permute(1, 0, 2), k)
 
 
 def distances_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int,

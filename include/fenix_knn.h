@@ -238,6 +238,23 @@ int fx_mask_compact_workspace_bytes(int64_t n, size_t* out_bytes);
 int fx_mask_compact(const uint32_t* mask, int64_t n, void* ws, size_t ws_bytes, int32_t* out_rows,
                     uint64_t* out_count, void* stream);
 
+/* ------------------------------------------------------ multi-GPU exchange
+ * Single-process communicator over RCCL (xGMI): one rank per listed device
+ * (a serving process driving every GPU of a node).  fx_allgather_topk gathers
+ * every rank's [nq][k] top-k list into every rank's all_dist/all_row
+ * [ndev][nq][k] buffers (one grouped call, each rank on its own stream);
+ * fx_topk_merge then reduces them.  Replaces the select over the concatenated
+ * sources of the reference (table.py:19-21 + index.py:166) when the shards
+ * live on several GPUs.  RCCL is loaded on first use (dlopen librccl.so.1);
+ * without it these return FX_EUNSUPPORTED.  Arrays of per-rank pointers are
+ * host arrays of device pointers; streams is a host array of hipStream_t.
+ */
+int fx_comm_init_all(int ndev, const int* devs, void** out_comm);
+int fx_comm_destroy(void* comm);
+int fx_allgather_topk(void* comm, const float* const* dist, const int64_t* const* row,
+                      int64_t nq, int64_t k, float* const* all_dist, int64_t* const* all_row,
+                      void* const* streams);
+
 #ifdef __cplusplus
 }
 #endif

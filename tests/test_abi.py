@@ -81,3 +81,19 @@ def test_metric_aliases_follow_coder():
     assert _lib.METRICS["euclidean"] == _lib.METRICS["l2"] == _lib.METRIC_L2
     assert _lib.METRICS["dot"] == _lib.METRICS["inner_product"] == _lib.METRIC_IP
     assert _lib.METRICS["cosine"] == _lib.METRIC_COS
+
+
+def test_comm_argument_checks_without_gpu():
+    """fx_comm_init_all rejects a device listed twice (one RCCL rank per
+    device) and an empty list before touching RCCL or the GPU."""
+    import ctypes
+
+    from fenix_amd import _lib
+
+    L = _lib.load()
+    h = ctypes.c_void_p()
+    two = (ctypes.c_int * 2)(0, 0)
+    assert L.fx_comm_init_all(2, two, ctypes.byref(h)) == -1
+    assert b"twice" in L.fx_last_error()
+    assert L.fx_comm_init_all(0, two, ctypes.byref(h)) == -1
+    assert L.fx_comm_destroy(None) == 0

@@ -421,3 +421,28 @@ def test_row_list_search_empty_and_all(eng):
                         [device_mask(one, eng.device)], [1])
     torch.cuda.synchronize()
     assert rr.cpu().numpy()[0, 0] == 1234 and np.all(rr.cpu().numpy()[0, 1:] == -1)
+
+
+# ---------------------------------------------------------------- RCCL exchange
+
+
+def test_rccl_allgather_single_device(eng):
+    """fx_comm_init_all / fx_allgather_topk with one rank (the box has one GPU;
+    the N-rank layout is [ndev][nq][k]) and the merge that follows."""
+    from fenix_amd.engine import DeviceComm
+
+    comm = DeviceComm([eng.device])
+    try:
+        d = torch.from_numpy(np.sort(np.random.RandomState(0).rand(3, 7).astype(np.float32), 1))
+        r = torch.arange(21, dtype=torch.int64).reshape(3, 7)
+        d, r = d.to(eng.device), r.to(eng.device)
+        (ad, ar), = comm.allgather([(d, r)])
+        torch.cuda.synchronize()
+        assert ad.shape == (1, 3, 7)
+        np.testing.assert_array_equal(ad[0].cpu().numpy(), d.cpu().numpy())
+        np.testing.assert_array_equal(ar[0].cpu().numpy(), r.cpu().numpy())
+        md, mr = comm.gather_merge([(d, r)], 5)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mr.cpu().numpy(), r.cpu().numpy()[:, :5])
+    finally:
+        comm.close()
