@@ -46,7 +46,8 @@ def parse():
     p.add_argument("--k", type=int, default=100)
     p.add_argument("--nq", type=int, default=1)
     p.add_argument("--metric", default="l2")
-    p.add_argument("--dtype", default="f32", choices=["f32", "f16"])
+    p.add_argument("--dtype", default="f32", choices=["f32", "f16", "qu8"],
+                   help="qu8: quint8 codes (ex/arrow/quint8), scanned by fx_knn_search_ex")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
@@ -66,6 +67,8 @@ def cpu_baseline(args):
     O.lib().fx_ref_fill(O._ptr(x), rows, args.d, 0, 0, 0)
     if args.dtype == "f16":
         x = x.astype(np.float16)
+    if args.dtype == "qu8":  # the CPU port scans the dequantised float32 values
+        x = O.dequantize(np.clip(np.rint(x / QU8_SCALE) + QU8_ZP, 0, 127), QU8_SCALE, QU8_ZP)
     q = O.fill_normal(1, args.d, 1)
     O.knn(x[: min(rows, 10000)], q, args.metric, args.k, precision=32, threads=threads)
     done, t0 = 0, time.perf_counter()
@@ -83,6 +86,12 @@ def cpu_baseline(args):
         "sample": f"{rows}x{args.d} {args.dtype} {args.metric} k={args.k}, {done} single-query "
         f"searches in {el:.1f}s (oracle/knn_ref.c precision=32, same generator)",
     }
+
+
+# quint8 bench corpus: the generator's N(0,1) rows coded with a fixed per-tensor
+# affine map over its range (|x| <= 2*sqrt(3)), codes 0..127 (reduce_range)
+QU8_SCALE = float(np.float32(4 * 3**0.5 / 127))
+QU8_ZP = 64
 
 
 def pmc_traffic(workload_tag):
@@ -121,17 +130,26 @@ def main():
     from fenix_amd.engine import Engine, Shard
 
     eng = Engine.get(device)
-    tdt = torch.float32 if args.dtype == "f32" else torch.float16
-    esize = 4 if args.dtype == "f32" else 2
+    qu8 = args.dtype == "qu8"
+    tdt = {"f32": torch.float32, "f16": torch.float16, "qu8": torch.uint8}[args.dtype]
+    esize = {"f32": 4, "f16": 2, "qu8": 1}[args.dtype]
     metric = _lib.METRICS[args.metric]
     n, d, k, nq = args.n, args.d, args.k, args.nq
     row_base = rank * n
     x = torch.empty((n, d), dtype=tdt, device=device)
-    eng.fill(x, seed=0, row_base=row_base)
-    qh = torch.empty((nq, d), dtype=tdt, device=device)
+    if qu8:  # synthetic codes: generator rows, quantised in 1M-row slices (data prep)
+        tmp = torch.empty((1_000_000, d), dtype=torch.float32, device=device)
+        for s in range(0, n, tmp.shape[0]):
+            m = min(tmp.shape[0], n - s)
+            eng.fill(tmp[:m], seed=0, row_base=row_base + s)
+            x[s : s + m] = torch.clamp(torch.round(tmp[:m] / QU8_SCALE) + QU8_ZP, 0, 127).to(tdt)
+        del tmp
+    else:
+        eng.fill(x, seed=0, row_base=row_base)
+    qh = torch.empty((nq, d), dtype=torch.float32 if qu8 else tdt, device=device)
     eng.fill(qh, seed=1)
     q = qh.to(torch.float32)
-    shard = Shard(x, row_base)
+    shard = Shard(x, row_base, QU8_SCALE, QU8_ZP) if qu8 else Shard(x, row_base)
     od = torch.empty((nq, k), dtype=torch.float32, device=device)
     orow = torch.empty((nq, k), dtype=torch.int64, device=device)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -140,10 +158,15 @@ def main():
     def step(i=None):
         if i is not None:
             ev[i][0].record()
-        ws = eng.scan(shard, q, metric, k)
+        if qu8:  # fx_knn_search_ex: scan + merge in one call (the merge is ~1 % of it)
+            with eng.lock:
+                eng.search_shard(shard, q, metric, k, None, od, orow)
+        else:
+            ws = eng.scan(shard, q, metric, k)
         if i is not None:
             ev[i][1].record()
-        eng.reduce(shard, q, metric, k, ws, od, orow)
+        if not qu8:
+            eng.reduce(shard, q, metric, k, ws, od, orow)
         if world > 1:
             if gloo:
                 gd, gr = allgather_topk(od.cpu(), orow.cpu())
@@ -205,7 +228,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "traffic": traffic,
-            "kernel": "fx::scan_kernel (fused distance + per-wave top-k)",
+            "kernel": "fx::scan_kernel<uint8> (quint8 codes dequantised in registers) + merge"
+            if qu8 else "fx::scan_kernel (fused distance + per-wave top-k)",
             "kernel_ms": scan_ms,
             "bytes_per_launch": scan_bytes,
         }

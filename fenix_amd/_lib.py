@@ -19,6 +19,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libfenix_knn.so")
 
 DTYPE_F32 = 0
 DTYPE_F16 = 1
+DTYPE_QU8 = 2  # quint8 codes (fx_knn_*_ex entry points)
 METRIC_L2 = 0
 METRIC_IP = 1
 METRIC_COS = 2
@@ -58,6 +59,9 @@ SYMBOLS = (
     "fx_knn_search_rows",
     "fx_mask_compact_workspace_bytes",
     "fx_mask_compact",
+    "fx_knn_search_ex_workspace_bytes",
+    "fx_knn_search_ex",
+    "fx_knn_distances_ex",
     "fx_comm_init_all",
     "fx_comm_destroy",
     "fx_allgather_topk",
@@ -65,6 +69,20 @@ SYMBOLS = (
 
 _lock = threading.Lock()
 _lib = None
+
+
+class Corpus(ctypes.Structure):
+    """struct fx_corpus (include/fenix_knn.h)."""
+
+    _fields_ = [
+        ("data", ctypes.c_void_p),
+        ("dtype", ctypes.c_int),
+        ("n", ctypes.c_int64),
+        ("d", ctypes.c_int64),
+        ("row_base", ctypes.c_int64),
+        ("scale", ctypes.c_float),
+        ("zero_point", ctypes.c_int32),
+    ]
 
 
 class FenixHipError(RuntimeError):
@@ -136,6 +154,13 @@ def load() -> ctypes.CDLL:
         L.fx_mask_compact_workspace_bytes.restype = ci
         L.fx_mask_compact.argtypes = [vp, i64, vp, sz, vp, vp, vp]
         L.fx_mask_compact.restype = ci
+        pc_ = ctypes.POINTER(Corpus)
+        L.fx_knn_search_ex_workspace_bytes.argtypes = [pc_, i64, i64, i64, psz]
+        L.fx_knn_search_ex_workspace_bytes.restype = ci
+        L.fx_knn_search_ex.argtypes = [pc_, vp, i64, vp, i64, ci, i64, vp, vp, sz, vp, vp, vp]
+        L.fx_knn_search_ex.restype = ci
+        L.fx_knn_distances_ex.argtypes = [pc_, vp, i64, ci, vp, vp, vp]
+        L.fx_knn_distances_ex.restype = ci
         L.fx_comm_init_all.argtypes = [ci, ctypes.POINTER(ci), ctypes.POINTER(vp)]
         L.fx_comm_init_all.restype = ci
         L.fx_comm_destroy.argtypes = [vp]
@@ -204,3 +229,10 @@ def search_rows_workspace_bytes(nrows: int, d: int, dtype: int, nq: int, k: int)
 
 def compact_workspace_bytes(n: int) -> int:
     return _ws(load().fx_mask_compact_workspace_bytes, n)
+
+
+def search_ex_workspace_bytes(corpus: "Corpus", nrows: int, nq: int, k: int) -> int:
+    out = ctypes.c_size_t(0)
+    check(load().fx_knn_search_ex_workspace_bytes(ctypes.byref(corpus), nrows, nq, k,
+                                                  ctypes.byref(out)))
+    return int(out.value)

@@ -24,6 +24,7 @@ struct ScanArgs {
   int mode;               // kModeTopk / kModeDist
   uint64_t* out_lists;    // topk: [nq][gridDim.x][k] composites (one list per block)
   float* out_dist;        // dist: [nq][n]
+  float qscale, qshift;   // FX_DTYPE_QU8: value = qscale * (code - qshift)
 };
 
 typedef void (*ScanKernelFn)(ScanArgs);

@@ -208,6 +208,7 @@ struct ScanCtx {
   int S, lane, grp, jl, qi;
   int64_t hi;
   float qnorm;
+  float qscale, qshift;  // uint8 codes: dequantised in registers
   bool topk;
 };
 
@@ -234,6 +235,8 @@ __device__ __forceinline__ void tile_load(RowTile<T, W, L, U>& t, int64_t it, in
       const int s = ch * 16 * L + cc * 16 + c.jl;
       if (t.valid[u] && s < c.S) {
         t.v[u][cc] = load_stream(rp + s);
+      } else if constexpr (sizeof(T) == 1) {
+        t.v[u][cc] = V((T)c.qshift);  // the zero-point code dequantises to exactly 0
       } else {
         t.v[u][cc] = V(0);
       }
@@ -255,7 +258,8 @@ __device__ __forceinline__ void tile_accumulate(const RowTile<T, W, L, U>& t, in
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int e = 0; e < W; ++e) {
-        const float x = elem<W>(t.v[u][cc], e);
+        float x = elem<W>(t.v[u][cc], e);
+        if constexpr (sizeof(T) == 1) x = c.qscale * (x - c.qshift);  // quint8 dequantise
         if constexpr (METRIC == 0) {
           const float d = x - qv[e];
           acc[u] = fmaf(d, d, acc[u]);
@@ -354,6 +358,8 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanArgs a) {
   c.jl = lane & 15;
   c.qi = qi;
   c.qnorm = 1.f;
+  c.qscale = a.qscale;
+  c.qshift = a.qshift;
   c.topk = a.mode == kModeTopk;
   if constexpr (METRIC == 2) {
     // F.normalize eps (coder.py:43-44): max(||q||, 1e-12); every wave reduces
@@ -488,6 +494,16 @@ ScanKernelFn select_scan_kernel(int dtype, int metric, int W, int L) {
     if (metric == 1) return pick_l<float, 4, 1>(L);
     return pick_l<float, 4, 2>(L);
   }
+  if (dtype == FX_DTYPE_QU8) {
+    if (W == 1) {
+      if (metric == 0) return pick_scalar<uint8_t, 0>();
+      if (metric == 1) return pick_scalar<uint8_t, 1>();
+      return pick_scalar<uint8_t, 2>();
+    }
+    if (metric == 0) return pick_l<uint8_t, 16, 0>(L);
+    if (metric == 1) return pick_l<uint8_t, 16, 1>(L);
+    return pick_l<uint8_t, 16, 2>(L);
+  }
   if (W == 1) {
     if (metric == 0) return pick_scalar<_Float16, 0>();
     if (metric == 1) return pick_scalar<_Float16, 1>();
@@ -501,7 +517,7 @@ ScanKernelFn select_scan_kernel(int dtype, int metric, int W, int L) {
 // Shape → kernel variant, LDS size, grid.  Pure function of (shape, device).
 int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool aligned,
               ScanPlan* p) {
-  const int vecw = dtype == FX_DTYPE_F32 ? 4 : 8;
+  const int vecw = dtype == FX_DTYPE_F32 ? 4 : dtype == FX_DTYPE_F16 ? 8 : 16;
   int W = (aligned && d % vecw == 0) ? vecw : 1;
   const int64_t S = d / W;
   int L;

@@ -44,8 +44,26 @@ def require_gpu() -> None:
         )
 
 
+def _is_quint8(t: pa.DataType) -> bool:
+    return isinstance(t, pa.ExtensionType) and t.extension_name == "tensor::qint8"
+
+
+def list_size(t: pa.DataType) -> int:
+    return (t.storage_type if isinstance(t, pa.ExtensionType) else t).list_size
+
+
+def qparams(t: pa.DataType) -> Tuple[float, int]:
+    """(scale, zero point) of a quint8 tensor column (ex/arrow/quint8); (1, 0) otherwise."""
+    if _is_quint8(t):
+        return float(t.scale), int(t.shift)
+    return 1.0, 0
+
+
 def value_dtype(t: pa.DataType) -> Tuple[int, torch.dtype, np.dtype]:
-    """fixed_size_list<float32|float16>[D] -> (C-ABI dtype, torch dtype, numpy dtype)."""
+    """fixed_size_list<float32|float16>[D] or a quint8 tensor column ->
+    (C-ABI dtype, torch dtype, numpy dtype)."""
+    if _is_quint8(t):
+        return _lib.DTYPE_QU8, torch.uint8, np.dtype(np.uint8)
     if not pa.types.is_fixed_size_list(t):
         raise TypeError(f"embedding column must be fixed_size_list<float>[D], got {t}")
     v = t.value_type
@@ -64,6 +82,8 @@ def _chunk_values(chunk: pa.FixedSizeListArray, np_dtype: np.dtype) -> np.ndarra
     the parent's array offset is honoured (from_arrow reads ``.values`` from
     element 0 even for a sliced array).
     """
+    if isinstance(chunk, pa.ExtensionArray):
+        chunk = chunk.storage
     d = chunk.type.list_size
     vals = chunk.values
     buf = vals.buffers()[1]
@@ -76,7 +96,7 @@ def stage_column(col: pa.ChunkedArray, device: torch.device) -> torch.Tensor:
     """Copy an Arrow fixed_size_list column into one contiguous [n, D] HBM tensor
     through pinned bounce buffers (one H2D copy per ~256 MB, not per chunk)."""
     _, tdt, ndt = value_dtype(col.type)
-    d = col.type.list_size
+    d = list_size(col.type)
     n = len(col)
     out = torch.empty((n, d), dtype=tdt, device=device)
     if n == 0:
@@ -121,8 +141,10 @@ def stage_column(col: pa.ChunkedArray, device: torch.device) -> torch.Tensor:
 class Shard:
     """One contiguous row range of the searched table, resident in HBM."""
 
-    data: torch.Tensor  # [n, D] float32 / float16
+    data: torch.Tensor  # [n, D] float32 / float16 / uint8 (quint8 codes)
     row_base: int  # global row of local row 0 (multi-source numbering, table.py:19-21)
+    scale: float = 1.0  # quint8: value = scale * (code - zero_point)
+    zero_point: int = 0
 
     @property
     def n(self) -> int:
@@ -134,7 +156,14 @@ class Shard:
 
     @property
     def dtype_id(self) -> int:
+        if self.data.dtype == torch.uint8:
+            return _lib.DTYPE_QU8
         return _lib.DTYPE_F32 if self.data.dtype == torch.float32 else _lib.DTYPE_F16
+
+    def corpus(self) -> "_lib.Corpus":
+        """struct fx_corpus for the _ex entry points."""
+        return _lib.Corpus(self.data.data_ptr(), self.dtype_id, self.n, self.d, self.row_base,
+                           self.scale, self.zero_point)
 
 
 @dataclass
@@ -256,6 +285,9 @@ class Engine:
                      out_row: torch.Tensor) -> None:
         """fx_knn_search on one shard.  queries [nq, D] f32 on device; caller holds lock."""
         nq = queries.shape[0]
+        if shard.dtype_id == _lib.DTYPE_QU8:
+            self._search_ex(shard, None, -1, queries, metric, k, mask, out_dist, out_row)
+            return
         nbytes = _lib.knn_workspace_bytes(shard.n, shard.d, shard.dtype_id, nq, k)
         ws = self._workspace(nbytes)
         _lib.check(
@@ -265,6 +297,17 @@ class Engine:
                 _ptr(out_dist), _ptr(out_row), self._stream(),
             )
         )
+
+    def _search_ex(self, shard: Shard, rows: Optional[torch.Tensor], nrows: int,
+                   queries: torch.Tensor, metric: int, k: int, mask: Optional[torch.Tensor],
+                   out_dist: torch.Tensor, out_row: torch.Tensor) -> None:
+        """fx_knn_search_ex (any dtype incl. quint8 codes, optional row list); caller holds lock."""
+        c = shard.corpus()
+        nq = queries.shape[0]
+        ws = self._workspace(_lib.search_ex_workspace_bytes(c, nrows, nq, k))
+        _lib.check(_lib.load().fx_knn_search_ex(
+            ctypes.byref(c), _ptr(rows), nrows, _ptr(queries), nq, metric, k, _ptr(mask),
+            _ptr(ws), ws.numel(), _ptr(out_dist), _ptr(out_row), self._stream()))
 
     def scan(self, shard: Shard, queries: torch.Tensor, metric: int, k: int,
              mask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -320,6 +363,9 @@ class Engine:
                     metric: int, k: int, out_dist: torch.Tensor, out_row: torch.Tensor) -> None:
         """fx_knn_search_rows over the listed local rows; caller holds lock."""
         nq = queries.shape[0]
+        if shard.dtype_id == _lib.DTYPE_QU8:
+            self._search_ex(shard, rows, nrows, queries, metric, k, None, out_dist, out_row)
+            return
         ws = self._workspace(_lib.search_rows_workspace_bytes(nrows, shard.d, shard.dtype_id, nq, k))
         _lib.check(_lib.load().fx_knn_search_rows(
             _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base, _ptr(rows), nrows,
@@ -374,6 +420,12 @@ class Engine:
         queries = queries.to(self.device, torch.float32).contiguous()
         out = torch.empty((queries.shape[0], shard.n), dtype=torch.float32, device=self.device)
         with self.lock:
+            if shard.dtype_id == _lib.DTYPE_QU8:
+                c = shard.corpus()
+                _lib.check(_lib.load().fx_knn_distances_ex(
+                    ctypes.byref(c), _ptr(queries), queries.shape[0], metric, _ptr(mask),
+                    _ptr(out), self._stream()))
+                return out
             _lib.check(
                 _lib.load().fx_knn_distances(
                     _ptr(shard.data), shard.dtype_id, shard.n, shard.d, _ptr(queries),

@@ -79,7 +79,8 @@ def shards(parts, column: str, devs) -> List[Tuple[_engine.Shard, int, int]]:
             pieces = _engine.CACHE.get(path, t, column, devs).pieces
         else:
             pieces = _engine.stage_sharded(t.column(column), devs)
-        out.extend((_engine.Shard(p.data, base + p.start), i, p.start)
+        scale, zp = _engine.qparams(t.schema.field(column).type)
+        out.extend((_engine.Shard(p.data, base + p.start, scale, zp), i, p.start)
                    for p in pieces if p.data.shape[0])
         base += t.num_rows
     return out

@@ -11,6 +11,8 @@ import os
 
 import pyarrow as pa
 
+from ..ex.arrow import quint8 as _quint8  # noqa: F401  (registers "tensor::qint8" for IPC reads)
+
 
 def load(path: str) -> pa.Table:
     with pa.memory_map(path, "rb") as source:

@@ -64,8 +64,36 @@ DIST_COL: str = "__DISTANCE__"
 LOCATION: str = "indexes"
 
 
+def _quint8_target(target, type: pa.DataType) -> np.ndarray:
+    """A quint8 tensor column (ex/arrow/quint8) is searched with a float target
+    of prod(shape) values (only the corpus is coded); a wrong length raises
+    ArrowInvalid like index.py:111's pa.scalar."""
+    if isinstance(target, pa.ChunkedArray):
+        target = target.combine_chunks()
+    if isinstance(target, pa.ExtensionScalar):
+        target = target.to_numpy().dequantize()
+    elif isinstance(target, pa.Scalar):
+        target = target.values.to_numpy(zero_copy_only=False)
+    elif isinstance(target, pa.Array):
+        target = target.to_numpy(zero_copy_only=False)
+    elif isinstance(target, Tensor):
+        target = target.numpy()
+    values = np.array(target, dtype=np.float32).ravel()
+    d = _engine.list_size(type)
+    if values.size != d:
+        raise pa.ArrowInvalid(f"target has {values.size} values, the column {d}")
+    return values.reshape(1, -1)
+
+
+def _dist_type(type: pa.DataType) -> pa.DataType:
+    """__DISTANCE__ has the column's value type (index.py:153-159); float32 for quint8."""
+    return pa.float32() if isinstance(type, pa.ExtensionType) else type.value_type
+
+
 def _target_values(target, type: pa.DataType) -> np.ndarray:
     """index.py:101-111: normalise the target and cast it to the column type."""
+    if isinstance(type, pa.ExtensionType):
+        return _quint8_target(target, type)
     if isinstance(target, pa.ChunkedArray):
         target = target.combine_chunks()
     if isinstance(target, pa.Array):
@@ -118,7 +146,7 @@ def _gather_vectors(shards, rows: np.ndarray, type: pa.DataType) -> pa.Array:
     """The k winning embeddings, read back from their HBM shards (they are the
     stored Arrow values, staged verbatim) instead of gathered from Arrow
     chunks: a few KB over PCIe instead of k chunk lookups."""
-    d = type.list_size
+    d = _engine.list_size(type)
     _, tdt, ndt = _engine.value_dtype(type)
     out = np.empty((rows.size, d), dtype=ndt)
     for s in shards:
@@ -126,6 +154,9 @@ def _gather_vectors(shards, rows: np.ndarray, type: pa.DataType) -> pa.Array:
         if sel.size:
             idx = torch.from_numpy(rows[sel] - s.row_base).to(s.data.device)
             out[sel] = s.data.index_select(0, idx).cpu().numpy()
+    if isinstance(type, pa.ExtensionType):  # quint8 codes: same type, same parameters
+        storage = pa.FixedSizeListArray.from_arrays(pa.array(out.ravel()), list_size=d)
+        return pa.ExtensionArray.from_storage(type, storage.cast(type.storage_type))
     return pa.FixedSizeListArray.from_arrays(pa.array(out.ravel()), list_size=d).cast(type)
 
 
@@ -389,5 +420,6 @@ def call(
             hm = host_mask()
             out = out.filter(pa.array(hm))
             dist = dist[hm]
-    out = out.append_column(DIST_COL, pa.array(dist.astype(type.value_type.to_pandas_dtype())))
+    dt = _dist_type(type)
+    out = out.append_column(DIST_COL, pa.array(dist.astype(dt.to_pandas_dtype()), type=dt))
     return out.select(select).combine_chunks()

@@ -42,6 +42,9 @@ extern "C" {
 /* dtype of the corpus (the Arrow fixed_size_list value type) */
 #define FX_DTYPE_F32 0
 #define FX_DTYPE_F16 1
+#define FX_DTYPE_QU8 2     /* uint8 codes, value = scale * (code - zero_point):
+                              the quint8 tensor column of ex/arrow/quint8/quint8.py:56-145;
+                              fx_knn_*_ex entry points only */
 
 /* metric; aliases are resolved by the host (coder.py:39 "euclidean"->l2,
  * coder.py:47 "dot"->inner_product) */
@@ -237,6 +240,32 @@ int fx_code_mask(const int64_t* row_code, int64_t n, const uint32_t* sel, int64_
 int fx_mask_compact_workspace_bytes(int64_t n, size_t* out_bytes);
 int fx_mask_compact(const uint32_t* mask, int64_t n, void* ws, size_t ws_bytes, int32_t* out_rows,
                     uint64_t* out_count, void* stream);
+
+/* ------------------------------------------------------ corpus descriptor
+ * The _ex entry points take the corpus as a descriptor, which also carries
+ * the dequantisation of FX_DTYPE_QU8 columns (per-tensor affine quint8,
+ * ex/arrow/quint8/quint8.py:56-58, 81-84: value = scale * (code - zero_point),
+ * computed in f32 exactly as QUInt8NDArray.dequantize does), and an optional
+ * row list (rows/nrows as in fx_knn_search_rows; rows == NULL: all n rows).
+ * The queries stay float32 (asymmetric distances: only the corpus is coded).
+ */
+typedef struct fx_corpus {
+  const void* data;    /* device, [n][d] of dtype */
+  int dtype;           /* FX_DTYPE_F32 / F16 / QU8 */
+  int64_t n, d;
+  int64_t row_base;    /* global row of row 0 */
+  float scale;         /* QU8 only */
+  int32_t zero_point;  /* QU8 only */
+} fx_corpus;
+
+int fx_knn_search_ex_workspace_bytes(const fx_corpus* c, int64_t nrows, int64_t nq, int64_t k,
+                                     size_t* out_bytes);
+int fx_knn_search_ex(const fx_corpus* c, const int32_t* rows, int64_t nrows,
+                     const float* queries, int64_t nq, int metric, int64_t k,
+                     const uint32_t* mask, void* ws, size_t ws_bytes, float* out_dist,
+                     int64_t* out_row, void* stream);
+int fx_knn_distances_ex(const fx_corpus* c, const float* queries, int64_t nq, int metric,
+                        const uint32_t* mask, float* out, void* stream);
 
 /* ------------------------------------------------------ multi-GPU exchange
  * Single-process communicator over RCCL (xGMI): one rank per listed device

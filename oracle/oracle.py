@@ -235,3 +235,9 @@ def distances(x: np.ndarray, q: np.ndarray, metric: str, precision: int = 64) ->
     if rc != 0:
         raise ValueError("fx_ref_distances failed")
     return out
+
+
+def dequantize(codes: np.ndarray, scale: float, shift: int) -> np.ndarray:
+    """quint8 codes -> float32 values exactly as QUInt8NDArray.dequantize
+    (src/fenix/ex/arrow/quint8/quint8.py:53-54): float32(scale) * (codes - shift)."""
+    return np.float32(scale) * (np.asarray(codes, dtype=np.float32) - np.float32(shift))

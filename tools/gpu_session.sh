@@ -25,6 +25,8 @@ for step in "$@"; do
     testcoder) run pytest_coder 900 python -u -m pytest tests/test_gpu_coder.py -m gpu -q -x -p no:cacheprovider ;;
     coded) run coded 600 python -u tools/bench_coded.py ;;
     profcoded) run profcoded 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profcoded -o run --output-format csv -- python3 -u tools/bench_coded.py --iters 3 ;;
+    testq8) run pytest_q8 600 python -u -m pytest tests/test_gpu_quint8.py -m gpu -q -x -p no:cacheprovider ;;
+    benchq8) run benchq8 600 python -u bench.py --dtype qu8 --steps 10 --warmup 2 ;;
     testk) run pytest_kernels 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_fullsize.py -m gpu -q -x -p no:cacheprovider ;;
     testsall) run pytest_gpu 1500 python -u -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python -u bench.py ;;
