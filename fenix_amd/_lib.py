@@ -15,7 +15,8 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libfenix_knn.so")
+LIB_PATH = os.environ.get("FENIX_AMD_LIB") or os.path.join(HERE, "lib", "libfenix_knn.so")
+# (FENIX_AMD_LIB: load a variant build instead, for tools/ A/B runs only)
 
 DTYPE_F32 = 0
 DTYPE_F16 = 1

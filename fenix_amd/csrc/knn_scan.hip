@@ -49,6 +49,32 @@
 #define FX_U12 1
 #endif
 
+// Rows in flight per group for quint8 rows (separately tunable).  Converted
+// codes take 4x their bytes in registers, so fewer rows per group and more
+// waves win: at 768-d (L = 3) U = 1 with 3 blocks/CU runs 1.77 ms vs 2.01 ms
+// for U = 2 with 2 (10M rows); U = 4 spills (13.9 ms).
+#ifndef FX_Q1
+#define FX_Q1 8
+#endif
+#ifndef FX_Q2
+#define FX_Q2 2
+#endif
+#ifndef FX_Q3
+#define FX_Q3 1
+#endif
+#ifndef FX_Q4
+#define FX_Q4 1
+#endif
+#ifndef FX_Q6
+#define FX_Q6 1
+#endif
+#ifndef FX_Q8
+#define FX_Q8 1
+#endif
+#ifndef FX_Q12
+#define FX_Q12 1
+#endif
+
 namespace fx {
 
 // ---------------------------------------------------------------- helpers --
@@ -248,6 +274,64 @@ template <typename T, int W, int L, int U, int METRIC>
 __device__ __forceinline__ void tile_accumulate(const RowTile<T, W, L, U>& t, int ch,
                                                 const ScanCtx& c, float (&acc)[U],
                                                 float (&acc2)[U]) {
+  if constexpr (sizeof(T) == 1) {
+    // quint8 codes, value = qscale * (code - qshift).  Per element: one
+    // ubyte->f32 convert and packed fp32 ops on pairs (v_pk_add/v_pk_fma):
+    //   L2   d = code - q'  with q' = qshift + q/qscale (query pre-transformed
+    //        in LDS), sum d^2;  distance = qscale * sqrt(sum)
+    //   IP   sum (code - qshift) q;            distance = -qscale * sum
+    //   cos  sum (code - qshift) q and (code - qshift)^2, scaled in tile_finish
+    // (vs dequantise-then-compute: 2-2.5 VALU ops per byte instead of 5-6; the
+    // scan was VALU-bound at 3.6 TB/s).
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef float f16v __attribute__((ext_vector_type(16)));
+    static_assert(W == 16 || W == 1, "quint8 rows are scanned 16 codes per lane");
+    const f2 z2 = {c.qshift, c.qshift};
+#pragma unroll
+    for (int cc = 0; cc < L; ++cc) {
+      const int s = ch * 16 * L + cc * 16 + c.jl;
+      if constexpr (W == 1) {
+        const float qv = c.q_lds[s];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float x = (float)t.v[u][cc];
+          if constexpr (METRIC == 0) {
+            const float d = x - qv;
+            acc[u] = fmaf(d, d, acc[u]);
+          } else {
+            const float d = x - c.qshift;
+            acc[u] = fmaf(d, qv, acc[u]);
+            if constexpr (METRIC == 2) acc2[u] = fmaf(d, d, acc2[u]);
+          }
+        }
+      } else {
+        f2 q2[8];
+        const f2* qp = reinterpret_cast<const f2*>(c.q_lds + s * W);
+#pragma unroll
+        for (int p = 0; p < 8; ++p) q2[p] = qp[p];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const f16v xf = __builtin_convertvector(t.v[u][cc], f16v);
+          f2 a2 = {0.f, 0.f}, b2 = {0.f, 0.f};
+#pragma unroll
+          for (int p = 0; p < 8; ++p) {
+            const f2 x2 = {xf[2 * p], xf[2 * p + 1]};
+            if constexpr (METRIC == 0) {
+              const f2 d = x2 - q2[p];
+              a2 = __builtin_elementwise_fma(d, d, a2);
+            } else {
+              const f2 d = x2 - z2;
+              a2 = __builtin_elementwise_fma(d, q2[p], a2);
+              if constexpr (METRIC == 2) b2 = __builtin_elementwise_fma(d, d, b2);
+            }
+          }
+          acc[u] += a2.x + a2.y;
+          if constexpr (METRIC == 2) acc2[u] += b2.x + b2.y;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int cc = 0; cc < L; ++cc) {
     const int s = ch * 16 * L + cc * 16 + c.jl;
@@ -258,8 +342,7 @@ __device__ __forceinline__ void tile_accumulate(const RowTile<T, W, L, U>& t, in
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int e = 0; e < W; ++e) {
-        float x = elem<W>(t.v[u][cc], e);
-        if constexpr (sizeof(T) == 1) x = c.qscale * (x - c.qshift);  // quint8 dequantise
+        const float x = elem<W>(t.v[u][cc], e);
         if constexpr (METRIC == 0) {
           const float d = x - qv[e];
           acc[u] = fmaf(d, d, acc[u]);
@@ -284,7 +367,17 @@ __device__ __forceinline__ void tile_finish(const RowTile<T, W, L, U>& t, float 
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const float s1 = sum16(acc[u]);
-    if constexpr (METRIC == 0) {
+    if constexpr (sizeof(T) == 1) {  // quint8: sums are in code units
+      if constexpr (METRIC == 0) {
+        dist[u] = c.qscale * sqrtf(s1);
+      } else if constexpr (METRIC == 1) {
+        dist[u] = -(c.qscale * s1);
+      } else {
+        const float s2 = sum16(acc2[u]);
+        const float nx = fmaxf(c.qscale * sqrtf(s2), 1e-12f);
+        dist[u] = 0.5f - 0.5f * ((c.qscale * s1) / (nx * c.qnorm));
+      }
+    } else if constexpr (METRIC == 0) {
       dist[u] = sqrtf(s1);
     } else if constexpr (METRIC == 1) {
       dist[u] = -s1;
@@ -344,7 +437,13 @@ __global__ void __launch_bounds__(256) scan_kernel(ScanArgs a) {
   float* q_lds = reinterpret_cast<float*>(smem);
   const int qi = blockIdx.y;
   const float* qg = a.q + (size_t)qi * a.d;
-  for (int i = threadIdx.x; i < qfl; i += 256) q_lds[i] = i < a.d ? qg[i] : 0.f;
+  for (int i = threadIdx.x; i < qfl; i += 256) {
+    float v = i < a.d ? qg[i] : 0.f;
+    // quint8 L2: q' = qshift + q / qscale (padding -> qshift, which the padded
+    // zero-point codes cancel exactly)
+    if constexpr (sizeof(T) == 1 && METRIC == 0) v = a.qshift + v / a.qscale;
+    q_lds[i] = v;
+  }
   __syncthreads();
 
   ScanCtx c;
@@ -452,22 +551,49 @@ constexpr bool kPipe = !(sizeof(T) == 2 && L >= 12);
 
 template <typename T, int W, int METRIC>
 static ScanKernelFn pick_l(int L) {
-  switch (L) {
-    case 1: return scan_kernel<T, W, 1, FX_U1, METRIC, kPipe<T, 1>>;
-    case 2: return scan_kernel<T, W, 2, FX_U2, METRIC, kPipe<T, 2>>;
-    case 3: return scan_kernel<T, W, 3, FX_U3, METRIC, kPipe<T, 3>>;
-    case 4: return scan_kernel<T, W, 4, FX_U4, METRIC, kPipe<T, 4>>;
-    case 6: return scan_kernel<T, W, 6, FX_U6, METRIC, kPipe<T, 6>>;
-    case 8: return scan_kernel<T, W, 8, FX_U8, METRIC, kPipe<T, 8>>;
-    case 12: return scan_kernel<T, W, 12, FX_U12, METRIC, kPipe<T, 12>>;
-    case 16: return scan_kernel<T, W, 16, 1, METRIC, kPipe<T, 16>>;
-    default: return scan_kernel<T, W, 24, 1, METRIC, kPipe<T, 24>>;
+  if constexpr (sizeof(T) == 1) {
+    switch (L) {
+      case 1: return scan_kernel<T, W, 1, FX_Q1, METRIC, true>;
+      case 2: return scan_kernel<T, W, 2, FX_Q2, METRIC, true>;
+      case 3: return scan_kernel<T, W, 3, FX_Q3, METRIC, true>;
+      case 4: return scan_kernel<T, W, 4, FX_Q4, METRIC, true>;
+      case 6: return scan_kernel<T, W, 6, FX_Q6, METRIC, true>;
+      case 8: return scan_kernel<T, W, 8, FX_Q8, METRIC, true>;
+      case 12: return scan_kernel<T, W, 12, FX_Q12, METRIC, true>;
+      case 16: return scan_kernel<T, W, 16, 1, METRIC, true>;
+      default: return scan_kernel<T, W, 24, 1, METRIC, true>;
+    }
+  } else {
+    switch (L) {
+      case 1: return scan_kernel<T, W, 1, FX_U1, METRIC, kPipe<T, 1>>;
+      case 2: return scan_kernel<T, W, 2, FX_U2, METRIC, kPipe<T, 2>>;
+      case 3: return scan_kernel<T, W, 3, FX_U3, METRIC, kPipe<T, 3>>;
+      case 4: return scan_kernel<T, W, 4, FX_U4, METRIC, kPipe<T, 4>>;
+      case 6: return scan_kernel<T, W, 6, FX_U6, METRIC, kPipe<T, 6>>;
+      case 8: return scan_kernel<T, W, 8, FX_U8, METRIC, kPipe<T, 8>>;
+      case 12: return scan_kernel<T, W, 12, FX_U12, METRIC, kPipe<T, 12>>;
+      case 16: return scan_kernel<T, W, 16, 1, METRIC, kPipe<T, 16>>;
+      default: return scan_kernel<T, W, 24, 1, METRIC, kPipe<T, 24>>;
+    }
   }
 }
 
 template <typename T, int METRIC>
 static ScanKernelFn pick_scalar() {
   return scan_kernel<T, 1, 16, 1, METRIC, true>;
+}
+
+static int rows_unroll_q8(int L) {
+  switch (L) {
+    case 1: return FX_Q1;
+    case 2: return FX_Q2;
+    case 3: return FX_Q3;
+    case 4: return FX_Q4;
+    case 6: return FX_Q6;
+    case 8: return FX_Q8;
+    case 12: return FX_Q12;
+    default: return 1;
+  }
 }
 
 static int rows_unroll(int L) {
@@ -534,7 +660,7 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
       }
     }
   }
-  const int U = W == 1 ? 1 : rows_unroll(L);
+  const int U = W == 1 ? 1 : dtype == FX_DTYPE_QU8 ? rows_unroll_q8(L) : rows_unroll(L);
   const int64_t CH = 16 * (int64_t)L;
   const int64_t nch = (S + CH - 1) / CH;
   const size_t qbytes = (size_t)((nch * CH * W * 4 + 15) / 16 * 16);
@@ -561,7 +687,7 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   // Two 256-thread blocks per CU already saturate HBM with the pipelined
   // tiles (sweep in profiles/), and fewer blocks mean fewer candidate lists
   // to merge.  FX_SCAN_BLOCKS_PER_CU overrides (tuning knob, microbench).
-  int cap_occ = 2;
+  int cap_occ = dtype == FX_DTYPE_QU8 ? 3 : 2;
   if (const char* env = getenv("FX_SCAN_BLOCKS_PER_CU")) cap_occ = atoi(env);
   if (cap_occ > 0 && cap_occ < occ) occ = cap_occ;
   if (occ < 1) occ = 1;
