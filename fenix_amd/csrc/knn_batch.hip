@@ -29,8 +29,11 @@
 
 namespace fx {
 
+#ifndef FX_BATCH_BQ
+#define FX_BATCH_BQ 256  // queries per block: 256 (110 KB LDS, 1 block/CU) or 128 (74 KB, 2)
+#endif
 constexpr int kBM = 128;        // rows per block tile
-constexpr int kBQ = 256;        // queries per block
+constexpr int kBQ = FX_BATCH_BQ;  // queries per block
 constexpr int kBK = 32;         // K chunk
 constexpr int kLds = kBK + 4;   // padded LDS row (floats)
 
@@ -50,19 +53,20 @@ __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<
 #endif
 constexpr int kWaves = FX_BATCH_WAVES;
 constexpr int kThreads = 64 * kWaves;
-constexpr int kQTiles = 8 * 4 / kWaves;  // 32-query MFMA tiles per wave
+constexpr int kQTiles = (kBQ / 32) * 4 / kWaves;  // 32-query MFMA tiles per wave
+constexpr int kBlocksPerCU = kBQ == 256 ? 1 : 2;
 
 // Stage one K chunk (columns [k0, k0+32)) of X rows [r0, r0+128) and of the
 // query tile into registers (16-B pieces; 1024 of X, 2048 of Q per chunk).
 struct Prefetch {
-  f32x4 x[1024 / kThreads];
-  f32x4 q[2048 / kThreads];
+  f32x4 x[kBM * 8 / kThreads];
+  f32x4 q[kBQ * 8 / kThreads];
 };
 
 __device__ __forceinline__ void prefetch_chunk(Prefetch& p, const BatchArgs& a, int64_t r0,
                                                int64_t q0, int k0, int tid) {
 #pragma unroll
-  for (int i = 0; i < 1024 / kThreads; ++i) {
+  for (int i = 0; i < kBM * 8 / kThreads; ++i) {
     const int idx = i * kThreads + tid;  // row = idx/8, col4 = idx%8
     const int row = idx >> 3, c4 = idx & 7;
     const int64_t gr = r0 + row;
@@ -75,7 +79,7 @@ __device__ __forceinline__ void prefetch_chunk(Prefetch& p, const BatchArgs& a, 
     }
   }
 #pragma unroll
-  for (int i = 0; i < 2048 / kThreads; ++i) {
+  for (int i = 0; i < kBQ * 8 / kThreads; ++i) {
     const int idx = i * kThreads + tid;  // query = idx/8, col4 = idx%8
     const int qq = idx >> 3, c4 = idx & 7;
     const int64_t gq = q0 + qq;
@@ -86,19 +90,20 @@ __device__ __forceinline__ void prefetch_chunk(Prefetch& p, const BatchArgs& a, 
 
 __device__ __forceinline__ void store_chunk(const Prefetch& p, BatchShared* sh, int buf, int tid) {
 #pragma unroll
-  for (int i = 0; i < 1024 / kThreads; ++i) {
+  for (int i = 0; i < kBM * 8 / kThreads; ++i) {
     const int idx = i * kThreads + tid;
     *reinterpret_cast<f32x4*>(&sh->xs[buf][(idx >> 3) * kLds + (idx & 7) * 4]) = p.x[i];
   }
 #pragma unroll
-  for (int i = 0; i < 2048 / kThreads; ++i) {
+  for (int i = 0; i < kBQ * 8 / kThreads; ++i) {
     const int idx = i * kThreads + tid;
     *reinterpret_cast<f32x4*>(&sh->qs[buf][(idx >> 3) * kLds + (idx & 7) * 4]) = p.q[i];
   }
 }
 
 template <int METRIC>
-__global__ void __launch_bounds__(kThreads, 1) batch_kernel(BatchArgs a) {
+// second argument: minimum waves per SIMD (kWaves * blocks per CU / 4 SIMDs)
+__global__ void __launch_bounds__(kThreads, kWaves * kBlocksPerCU / 4) batch_kernel(BatchArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   BatchShared* sh = reinterpret_cast<BatchShared*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -210,7 +215,7 @@ int launch_batch(const BatchArgs& a, int metric, hipStream_t stream) {
   int rc = device_cus(&cus);
   if (rc) return rc;
   const int64_t qtiles = (a.nq + kBQ - 1) / kBQ;
-  int64_t bx = cus;
+  int64_t bx = (int64_t)cus * kBlocksPerCU;
   if (bx > a.num_tiles) bx = a.num_tiles;
   for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
     BatchArgs b = a;

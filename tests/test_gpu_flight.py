@@ -223,3 +223,27 @@ def test_remove(env):
     import os
 
     assert not os.path.exists(env["root"])
+
+
+def test_concurrent_searches_match_sequential(env):
+    """Flight handlers run on several gRPC threads at once (the reference has no
+    locking, flight.py:62-77): 8 client threads searching together get exactly
+    the results they get one at a time."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    port = env["flight"].port
+    targets = O.fill_normal(16, VECTOR_SIZE, seed=36)
+    metrics = ["l2", "cosine", "dot", "euclidean"]
+
+    def one(i):
+        f = fenix_amd.Flight(host="127.0.0.1", port=port)
+        r = f.search(target=targets[i], source="test/table", column="vector",
+                     metric=metrics[i % 4], select=["id"], maxval=20 + i)
+        return r.column("id").to_numpy(), r.column("__DISTANCE__").to_numpy()
+
+    seq = [one(i) for i in range(16)]
+    with ThreadPoolExecutor(8) as pool:
+        par = list(pool.map(one, range(16)))
+    for (a, da), (b, db) in zip(seq, par):
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(da, db)
