@@ -217,14 +217,6 @@ def test_registered_distance_udf(env):
         assert np.all(np.abs(got - ref) <= 1e-5 * scale)
 
 
-def test_remove(env):
-    flight = env["flight"]
-    flight.remove()
-    import os
-
-    assert not os.path.exists(env["root"])
-
-
 def test_concurrent_searches_match_sequential(env):
     """Flight handlers run on several gRPC threads at once (the reference has no
     locking, flight.py:62-77): 8 client threads searching together get exactly
@@ -247,3 +239,12 @@ def test_concurrent_searches_match_sequential(env):
     for (a, da), (b, db) in zip(seq, par):
         np.testing.assert_array_equal(a, b)
         np.testing.assert_array_equal(da, db)
+
+
+def test_remove(env):
+    flight = env["flight"]
+    flight.remove()
+    import os
+
+    assert not os.path.exists(env["root"])
+
