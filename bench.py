@@ -85,7 +85,39 @@ def cpu_baseline(args):
         "kind": "port",
         "sample": f"{rows}x{args.d} {args.dtype} {args.metric} k={args.k}, {done} single-query "
         f"searches in {el:.1f}s (oracle/knn_ref.c precision=32, same generator)",
+        "reference_algorithm": torch_cpu_baseline(args, x, q, threads),
     }
+
+
+def torch_cpu_baseline(args, x, q, threads):
+    """The reference's own arithmetic on the CPU: coder.distance (torch.cdist /
+    -u@v.T / normalised matmul, src/fenix/io/coder/coder.py:38-50) over the
+    sample + torch.topk in place of select_k_unstable (index.py:166), without
+    the per-chunk Arrow UDF and Table.take overheads the reference adds."""
+    xt = torch.from_numpy(np.asarray(x, dtype=np.float32))
+    qt = torch.from_numpy(np.asarray(q, dtype=np.float32))
+    torch.set_num_threads(threads)
+
+    def one():
+        if args.metric in ("l2", "euclidean"):
+            d = torch.cdist(qt, xt)
+        elif args.metric == "cosine":
+            d = 0.5 - 0.5 * torch.nn.functional.normalize(qt, dim=-1) @ \
+                torch.nn.functional.normalize(xt, dim=-1).T
+        else:
+            d = -qt @ xt.T
+        return torch.topk(d, args.k, largest=False)
+
+    one()
+    done, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds / 2:
+            break
+    return {"value": x.shape[0] * done / el, "unit": "vectors/s", "cores": threads,
+            "sample": f"same sample, torch {torch.__version__} CPU, {done} searches in {el:.1f}s"}
 
 
 # quint8 bench corpus: the generator's N(0,1) rows coded with a fixed per-tensor
