@@ -28,6 +28,7 @@ for step in "$@"; do
     testq8) run pytest_q8 600 python -u -m pytest tests/test_gpu_quint8.py -m gpu -q -x -p no:cacheprovider ;;
     benchq8) run benchq8 600 python -u bench.py --dtype qu8 --steps 10 --warmup 2 ;;
     benchq8all) run benchq8ip 300 python -u bench.py --dtype qu8 --steps 10 --warmup 2 --metric inner_product --no-cpu-baseline && run benchq8cos 300 python -u bench.py --dtype qu8 --steps 10 --warmup 2 --metric cosine --no-cpu-baseline ;;
+    profq8) run profq8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profq8 -o run --output-format csv -- python3 -u bench.py --dtype qu8 --steps 10 --warmup 2 --no-cpu-baseline ;;
     testk) run pytest_kernels 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_fullsize.py -m gpu -q -x -p no:cacheprovider ;;
     testsall) run pytest_gpu 1500 python -u -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python -u bench.py ;;
