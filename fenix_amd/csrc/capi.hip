@@ -101,7 +101,8 @@ static int validate(int64_t n, int64_t d, int dtype, int64_t nq, int metric) {
   return FX_OK;
 }
 
-static constexpr int64_t kMaxK = 1024;
+static constexpr int64_t kMaxK = 1024;  // fused path; larger k: knn_large.hip
+static constexpr int64_t kLargeMaxK = 0x7fffffffll;
 
 // ---------------------------------------------------------------- batched --
 //
@@ -185,6 +186,8 @@ struct SearchLayout {
   ScanPlan scan;
   MergePlan merge;
   size_t lists_bytes, total;
+  bool large = false;  // k > kMaxK: distance-mode scan + radix sort (knn_large.hip)
+  LargeLayout lg;
   bool batched;
   BatchLayout batch;
   size_t single_off;  // batched: workspace of the single-query fallback
@@ -202,8 +205,21 @@ static int plan_single(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, i
   return FX_OK;
 }
 
+static int plan_large_search(int64_t n, int64_t d, int dtype, int64_t nq, int metric,
+                             bool aligned, SearchLayout* s) {
+  int rc = plan_scan(n, d, dtype, 1, metric, aligned, &s->scan);
+  if (rc) return rc;
+  s->large = true;
+  s->batched = false;
+  s->lg = plan_large(n, nq);
+  s->lists_bytes = 0;
+  s->total = s->lg.total;
+  return FX_OK;
+}
+
 static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
                        bool aligned, SearchLayout* s) {
+  if (k > kMaxK) return plan_large_search(n, d, dtype, nq, metric, aligned, s);
   if (!use_batched(nq, dtype, metric, d, aligned)) {
     return plan_single(n, d, dtype, nq, k, metric, aligned, s);
   }
@@ -328,8 +344,8 @@ int fx_knn_workspace_bytes(int64_t n, int64_t d, int dtype, int64_t nq, int64_t 
   }
   int rc = validate(n, d, dtype, nq, 0);
   if (rc) return rc;
-  if (k < 1 || k > kMaxK) {
-    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kMaxK);
+  if (k < 1 || k > kLargeMaxK) {
+    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kLargeMaxK);
     return FX_EUNSUPPORTED;
   }
   size_t best = 0;
@@ -349,8 +365,8 @@ static int search_layout(const void* corpus, int dtype, int64_t n, int64_t d, in
                          int metric, int64_t k, void* ws, size_t ws_bytes, SearchLayout* s) {
   int rc = validate(n, d, dtype, nq, metric);
   if (rc) return rc;
-  if (k < 1 || k > kMaxK) {
-    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kMaxK);
+  if (k < 1 || k > kLargeMaxK) {
+    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kLargeMaxK);
     return FX_EUNSUPPORTED;
   }
   if (!corpus || !ws) {
@@ -387,6 +403,19 @@ int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row
     return batched_phases(s.batch, reinterpret_cast<const float*>(corpus), n, d, row_base,
                           queries, nq, metric, k, mask, reinterpret_cast<char*>(ws), st);
   }
+  if (s.large) {
+    ScanArgs a = {};
+    a.X = corpus;
+    a.n = n;
+    a.d = (int)d;
+    a.row_base = row_base;
+    a.mask = mask;
+    a.rows_per_block = s.scan.rows_per_block;
+    a.cap = s.scan.cap;
+    a.qbytes = s.scan.qbytes;
+    a.q = queries;
+    return large_scan(s.scan, a, nq, s.lg, reinterpret_cast<char*>(ws), st);
+  }
   uint64_t* lists = reinterpret_cast<uint64_t*>(ws);
   ScanArgs a = {};
   a.X = corpus;
@@ -421,6 +450,9 @@ int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
     return FX_EINVAL;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (s.large) {
+    return large_reduce(n, nq, k, s.lg, reinterpret_cast<char*>(ws), out_dist, out_row, st);
+  }
   if (!s.batched) {
     const uint64_t* lists = reinterpret_cast<const uint64_t*>(ws);
     void* mws = reinterpret_cast<char*>(ws) + s.lists_bytes;
@@ -478,12 +510,13 @@ int fx_knn_search_rows_workspace_bytes(int64_t nrows, int64_t d, int dtype, int6
   }
   int rc = validate(nrows, d, dtype, nq, FX_METRIC_L2);
   if (rc) return rc;
-  if (k < 1 || k > kMaxK) {
-    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kMaxK);
+  if (k < 1 || k > kLargeMaxK) {
+    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kLargeMaxK);
     return FX_EUNSUPPORTED;
   }
   SearchLayout s;
-  rc = plan_single(nrows, d, dtype, nq, k, FX_METRIC_L2, true, &s);
+  rc = k > kMaxK ? plan_large_search(nrows, d, dtype, nq, FX_METRIC_L2, true, &s)
+                 : plan_single(nrows, d, dtype, nq, k, FX_METRIC_L2, true, &s);
   if (rc) return rc;
   *out_bytes = s.total;
   return FX_OK;
@@ -495,8 +528,8 @@ int fx_knn_search_rows(const void* corpus, int dtype, int64_t n, int64_t d, int6
                        int64_t* out_row, void* stream) {
   int rc = validate(nrows, d, dtype, nq, metric);
   if (rc) return rc;
-  if (k < 1 || k > kMaxK) {
-    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kMaxK);
+  if (k < 1 || k > kLargeMaxK) {
+    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kLargeMaxK);
     return FX_EUNSUPPORTED;
   }
   if (!corpus || !ws || !queries || !out_dist || !out_row || (nrows > 0 && !rows)) {
@@ -509,13 +542,30 @@ int fx_knn_search_rows(const void* corpus, int dtype, int64_t n, int64_t d, int6
     return FX_EUNSUPPORTED;
   }
   SearchLayout s;
-  rc = plan_single(nrows, d, dtype, nq, k, metric, ((uintptr_t)corpus % 16) == 0, &s);
+  const bool aligned = ((uintptr_t)corpus % 16) == 0;
+  rc = k > kMaxK ? plan_large_search(nrows, d, dtype, nq, metric, aligned, &s)
+                 : plan_single(nrows, d, dtype, nq, k, metric, aligned, &s);
   if (rc) return rc;
   if (ws_bytes < s.total) {
     set_error("workspace too small: %zu < %zu", ws_bytes, s.total);
     return FX_EINVAL;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (s.large) {
+    ScanArgs a = {};
+    a.X = corpus;
+    a.n = nrows;
+    a.d = (int)d;
+    a.row_base = row_base;
+    a.rows = rows;
+    a.rows_per_block = s.scan.rows_per_block;
+    a.cap = s.scan.cap;
+    a.qbytes = s.scan.qbytes;
+    a.q = queries;
+    rc = large_scan(s.scan, a, nq, s.lg, reinterpret_cast<char*>(ws), st);
+    if (rc) return rc;
+    return large_reduce(nrows, nq, k, s.lg, reinterpret_cast<char*>(ws), out_dist, out_row, st);
+  }
   uint64_t* lists = reinterpret_cast<uint64_t*>(ws);
   ScanArgs a = {};
   a.X = corpus;
@@ -574,11 +624,19 @@ int fx_knn_distances(const void* corpus, int dtype, int64_t n, int64_t d,
   return FX_OK;
 }
 
+// merges of lists longer than the fused path's k go through the radix sort
+static bool merge_is_large(int64_t kin, int64_t k) { return k > kMaxK || kin > kMaxK; }
+
 int fx_topk_merge_workspace_bytes(int64_t nq, int64_t parts, int64_t kin, int64_t k,
                                   size_t* out_bytes) {
-  if (!out_bytes || nq < 1 || parts < 1 || kin < 1 || k < 1 || k > kMaxK) {
+  if (!out_bytes || nq < 1 || parts < 1 || kin < 1 || k < 1 || k > kLargeMaxK ||
+      parts * kin > kLargeMaxK) {
     set_error("invalid merge shape");
     return FX_EINVAL;
+  }
+  if (merge_is_large(kin, k)) {
+    *out_bytes = plan_large(parts * kin, nq).total;
+    return FX_OK;
   }
   MergePlan mp;
   int rc = plan_merge(nq, parts, kin, k, &mp);
@@ -601,10 +659,18 @@ int fx_topk_merge(const float* in_dist, const int64_t* in_row, int64_t nq, int64
     set_error("workspace too small: %zu < %zu", ws_bytes, need);
     return FX_EINVAL;
   }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (merge_is_large(kin, k)) {
+    const LargeLayout l = plan_large(parts * kin, nq);
+    char* w = reinterpret_cast<char*>(ws);
+    rc = launch_encode(in_dist, in_row, nq * parts * kin,
+                       reinterpret_cast<uint64_t*>(w + l.off_keys), st);
+    if (rc) return rc;
+    return large_reduce(parts * kin, nq, k, l, w, out_dist, out_row, st);
+  }
   MergePlan mp;
   rc = plan_merge(nq, parts, kin, k, &mp);
   if (rc) return rc;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   uint64_t* comp = reinterpret_cast<uint64_t*>(ws);
   void* mws = reinterpret_cast<char*>(ws) + align256((size_t)nq * parts * kin * 8);
   rc = launch_encode(in_dist, in_row, nq * parts * kin, comp, st);

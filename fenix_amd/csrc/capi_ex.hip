@@ -8,7 +8,7 @@
 namespace fx {
 namespace {
 
-constexpr int64_t kMaxKEx = 1024;
+constexpr int64_t kMaxKEx = 1024;  // fused path; larger k: knn_large.hip
 
 size_t align256(size_t v) { return (v + 255) / 256 * 256; }
 
@@ -51,14 +51,25 @@ struct ExPlan {
   ScanPlan scan;
   MergePlan merge;
   size_t lists_bytes, total;
+  bool large = false;
+  LargeLayout lg;
 };
 
 int plan_ex(const fx_corpus* c, int64_t rows, int64_t nq, int64_t k, int metric, ExPlan* p) {
-  if (k < 1 || k > kMaxKEx) {
-    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kMaxKEx);
+  if (k < 1 || k > 0x7fffffffll) {
+    set_error("k=%lld out of range", (long long)k);
     return FX_EUNSUPPORTED;
   }
-  int rc = plan_scan(rows, c->d, c->dtype, k, metric, ((uintptr_t)c->data % 16) == 0, &p->scan);
+  const bool aligned = ((uintptr_t)c->data % 16) == 0;
+  if (k > kMaxKEx) {
+    int rc = plan_scan(rows, c->d, c->dtype, 1, metric, aligned, &p->scan);
+    if (rc) return rc;
+    p->large = true;
+    p->lg = plan_large(rows, nq);
+    p->total = p->lg.total;
+    return FX_OK;
+  }
+  int rc = plan_scan(rows, c->d, c->dtype, k, metric, aligned, &p->scan);
   if (rc) return rc;
   rc = plan_merge(nq, p->scan.nlists, k, k, &p->merge);
   if (rc) return rc;
@@ -130,6 +141,16 @@ int fx_knn_search_ex(const fx_corpus* c, const int32_t* rows, int64_t nrows,
     return FX_EINVAL;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (p.large) {
+    ScanArgs a = base_args(c, p.scan);
+    a.n = n;
+    a.rows = rows;
+    a.mask = mask;
+    a.q = queries;
+    rc = large_scan(p.scan, a, nq, p.lg, reinterpret_cast<char*>(ws), st);
+    if (rc) return rc;
+    return large_reduce(n, nq, k, p.lg, reinterpret_cast<char*>(ws), out_dist, out_row, st);
+  }
   uint64_t* lists = reinterpret_cast<uint64_t*>(ws);
   ScanArgs a = base_args(c, p.scan);
   a.n = n;

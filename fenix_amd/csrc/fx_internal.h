@@ -84,4 +84,15 @@ int check_launch(const char* what);
 int device_cus(int* out);
 int kernel_occupancy(const void* fn, int block, size_t smem, int* out);
 
+// k above the fused path (knn_large.hip): all distances + radix sort.
+struct LargeLayout {
+  size_t off_dist, off_keys, off_sorted, off_temp, temp_bytes, total;
+};
+LargeLayout plan_large(int64_t n, int64_t nq);
+// distances (distance-mode scan with plan p) + composites into ws
+int large_scan(const ScanPlan& p, ScanArgs a, int64_t nq, const LargeLayout& l, char* ws,
+               hipStream_t st);
+int large_reduce(int64_t n, int64_t nq, int64_t k, const LargeLayout& l, char* ws,
+                 float* out_dist, int64_t* out_row, hipStream_t st);
+
 }  // namespace fx

@@ -67,7 +67,11 @@ const char* fx_last_error(void);
 /* Number of visible HIP devices. */
 int fx_device_count(int* out);
 
-/* Largest k accepted by fx_knn_search. */
+/* Largest k of the fused scan + merge path (1024).  Any larger k (the
+ * reference's maxval is unbounded, index.py:165-168) is served by a
+ * distance-mode scan + radix sort of all n composites (knn_large.hip): every
+ * search entry point and fx_topk_merge accept k up to 2^31 - 1, with the same
+ * ordering contract, at the cost of n*nq*20 bytes of workspace. */
 int64_t fx_max_k(void);
 
 /*

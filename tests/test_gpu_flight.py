@@ -241,6 +241,17 @@ def test_concurrent_searches_match_sequential(env):
         np.testing.assert_array_equal(da, db)
 
 
+def test_maxval_above_fused_k(env):
+    """maxval = 2 500 (> the fused path's 1 024): same rows as the oracle."""
+    target = O.fill_normal(1, VECTOR_SIZE, seed=37)[0]
+    r = env["flight"].search(target=target, source="test/table", column="vector", metric="l2",
+                             select=["id"], maxval=2500)
+    assert r.num_rows == 2500
+    od, orow = O.knn(env["x"], target[None], "l2", 2500)
+    check_topk(r.column("__DISTANCE__").to_numpy()[None], r.column("id").to_numpy()[None], od,
+               orow, env["x"], target[None], "l2")
+
+
 def test_remove(env):
     flight = env["flight"]
     flight.remove()

@@ -295,7 +295,7 @@ def test_error_paths(eng):
     x = gpu_fill(eng, 10, 8, seed=1)
     q = torch.zeros((1, 8), device=eng.device)
     with pytest.raises(NotImplementedError):
-        eng.search([Shard(x, 0)], q, 0, _lib.max_k() + 1)
+        eng.search([Shard(x, 0)], q, 0, 1 << 31)
     with pytest.raises(ValueError):
         eng.search([Shard(x, 0)], q, 7, 5)
 
@@ -446,3 +446,48 @@ def test_rccl_allgather_single_device(eng):
         np.testing.assert_array_equal(mr.cpu().numpy(), r.cpu().numpy()[:, :5])
     finally:
         comm.close()
+
+
+# ---------------------------------------------------------------- k > 1024
+
+
+@pytest.mark.parametrize("metric", METRICS)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_large_k_sorted_path(eng, metric, dtype):
+    """k above the fused path's 1024 (the reference's maxval is unbounded):
+    distance-mode scan + radix sort, same results as the oracle."""
+    n, d, k = 20_000, 64, 3000
+    x = gpu_fill(eng, n, d, seed=81, dtype=dtype)
+    q = O.fill_normal(3, d, seed=82)
+    xh = O.fill_normal(n, d, 81, dtype=np.float32 if dtype == torch.float32 else np.float16)
+    xh = xh.astype(np.float32)
+    gd, gr = gpu_search(eng, x, q, metric, k, row_base=0)
+    od, orow = O.knn(xh, q, metric, k)
+    check_topk(gd, gr, od, orow, xh, q, metric)
+    keep = np.random.RandomState(2).rand(n) < 0.3  # masked; < 50 %: row-list path
+    gd, gr = gpu_search(eng, x, q, metric, 2500, mask=keep)
+    od, orow = O.knn(xh, q, metric, 2500, mask=keep)
+    check_topk(gd, gr, od, orow, xh, q, metric)
+    m = device_mask(keep, eng.device)
+    d2, r2 = eng.search([Shard(x, 0)], torch.from_numpy(q).to(eng.device), _lib.METRICS[metric],
+                        2500, [m], [int(keep.sum())])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(r2.cpu().numpy(), gr)
+
+
+def test_large_k_exceeding_rows_and_multi_shard_merge(eng):
+    n, d = 1500, 32
+    x = gpu_fill(eng, n, d, seed=83)
+    q = O.fill_normal(1, d, seed=84)
+    gd, gr = gpu_search(eng, x, q, "l2", 2000)
+    assert np.all(gr[0, n:] == -1) and np.all(np.isnan(gd[0, n:]))
+    np.testing.assert_array_equal(np.sort(gr[0, :n]), np.arange(n))
+    # three shards, k = 2500 > each shard: merged by the sort-based fx_topk_merge
+    big = gpu_fill(eng, 9000, d, seed=85)
+    shards = [Shard(big[0:3000], 0), Shard(big[3000:6000], 3000), Shard(big[6000:], 6000)]
+    qt = torch.from_numpy(q).to(eng.device)
+    dd, rr = eng.search(shards, qt, _lib.METRIC_IP, 2500)
+    torch.cuda.synchronize()
+    od, orow = O.knn(O.fill_normal(9000, d, 85), q, "inner_product", 2500)
+    check_topk(dd.cpu().numpy(), rr.cpu().numpy(), od, orow, O.fill_normal(9000, d, 85), q,
+               "inner_product")
