@@ -424,8 +424,14 @@ __device__ __forceinline__ void tile_consume(const RowTile<T, W, L, U>& t, const
   tile_finish<T, W, L, U, METRIC>(t, acc, acc2, c, thr, cnt);
 }
 
+#ifndef FX_Q8_WAVES
+#define FX_Q8_WAVES 1  // minimum waves per SIMD for the quint8 kernels (4: <= 128 VGPRs)
+#endif
+template <typename T>
+constexpr int kMinWaves = sizeof(T) == 1 ? FX_Q8_WAVES : 1;
+
 template <typename T, int W, int L, int U, int METRIC, bool PIPE>
-__global__ void __launch_bounds__(256) scan_kernel(ScanArgs a) {
+__global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
