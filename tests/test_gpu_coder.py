@@ -298,6 +298,20 @@ def test_probe_search_filter_select_and_whole(fl_env):
     assert r3.equals(r)
 
 
+def test_coding_without_probes_is_brute_force_with_codes(fl_env):
+    """coding given, probes None (index.py:93-96, 113 not taken): the joined
+    table is searched exhaustively; the code column rides along."""
+    root = fl_env["root"]
+    target = O.fill_normal(1, VECTOR_SIZE, seed=54)[0]
+    r = index.call(root, "test/l2", "test/table", "vector", target=target, metric="cosine",
+                   maxval=12)
+    assert r.schema.names == ["id", "vector", "__CODED_ID__", "__DISTANCE__"]
+    od, orow = O.knn(fl_env["x"], target[None], "cosine", 12)
+    np.testing.assert_array_equal(r.column("id").to_numpy(), orow[0])
+    codes = index.load(root, "test/l2", "test/table", "vector").column("__CODED_ID__").to_numpy()
+    np.testing.assert_array_equal(r.column("__CODED_ID__").to_numpy(), codes[orow[0]])
+
+
 def test_drop_index(fl_env):
     root = fl_env["root"]
     flight = fl_env["flight"]

@@ -252,6 +252,22 @@ def test_maxval_above_fused_k(env):
                orow, env["x"], target[None], "l2")
 
 
+def test_empty_source(env):
+    """A source with no rows: the reference returns an empty table with the
+    output schema (index.py:165 not taken); so does the GPU path."""
+    empty = pa.Table.from_batches([], SCHEMA)
+    env["flight"].make_table("test/empty", empty.to_reader())
+    t = O.fill_normal(1, VECTOR_SIZE, seed=38)[0]
+    r = env["flight"].search(target=t, source="test/empty", column="vector", metric="l2",
+                             maxval=10)
+    assert r.num_rows == 0
+    assert r.schema == pa.schema([*SCHEMA, pa.field("__DISTANCE__", pa.float32())])
+    both = index.call(env["root"], None, ["test/empty", "test/table"], "vector", target=t,
+                      metric="l2", select=["id"], maxval=5)
+    od, orow = O.knn(env["x"], t[None], "l2", 5)
+    np.testing.assert_array_equal(both.column("id").to_numpy(), orow[0])
+
+
 def test_remove(env):
     flight = env["flight"]
     flight.remove()
