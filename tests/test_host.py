@@ -207,3 +207,15 @@ def test_index_files_list_and_drop(tmp_path):
     assert sorted(index.list(root)) == ["a/b/vector/c/l2", "t/v/dot"]
     index.drop(root, "dot", "t", "v")
     assert list(index.list(root)) == ["a/b/vector/c/l2"]
+
+
+def test_launcher_cli_help():
+    """fenix_amd.launch mirrors src/fenix/launch.py (root, --host, --port)."""
+    import subprocess
+    import sys
+
+    out = subprocess.run([sys.executable, "-m", "fenix_amd.launch", "--help"], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0
+    for opt in ("--host", "--port", "--devices"):
+        assert opt in out.stdout
