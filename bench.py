@@ -239,7 +239,7 @@ def main():
     tag = f"{n}x{d}_{args.dtype}_{args.metric}_k{k}_q{nq}"
     traffic = pmc_traffic(tag)
     # batched inner-product / cosine queries run on the fp32 matrix cores
-    mfma = nq >= 8 and args.dtype == "f32" and metric in (_lib.METRIC_IP, _lib.METRIC_COS)
+    mfma = nq >= 8 and args.dtype == "f32"
     if mfma:
         flops = 2.0 * n * nq * d
         roof = {

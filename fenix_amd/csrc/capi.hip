@@ -106,8 +106,10 @@ static constexpr int64_t kLargeMaxK = 0x7fffffffll;
 
 // ---------------------------------------------------------------- batched --
 //
-// Batched queries (nq >= kBatchMinQ, f32, inner product / cosine) run the
-// MFMA kernel of knn_batch.hip in phases over growing row samples:
+// Batched queries (nq >= kBatchMinQ, f32) run the MFMA kernel of knn_batch.hip
+// in phases over growing row samples (L2: the GEMM gives |x|^2+|q|^2-2x.q,
+// rows pass on a rigorous fp32 lower bound and every appended candidate is
+// rescored exactly before any threshold or result is taken):
 //   phase 0: a sample of <= cap rows, no threshold -> every (row, query) kept;
 //   phase i: a sample ~cap/(4k) times larger, threshold = the k-th composite
 //            of phase i-1 (an upper bound of the global k-th: the k-th of any
@@ -130,8 +132,7 @@ static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool align
   if (const char* env = getenv("FX_BATCH")) {
     if (atoi(env) == 0) return false;
   }
-  return nq >= kBatchMinQ && dtype == FX_DTYPE_F32 &&
-         (metric == FX_METRIC_IP || metric == FX_METRIC_COS) && d % 4 == 0 && aligned;
+  return nq >= kBatchMinQ && dtype == FX_DTYPE_F32 && d % 4 == 0 && aligned;
 }
 
 static int plan_batched(int64_t n, int64_t nq, int64_t k, BatchLayout* b) {
@@ -274,8 +275,12 @@ static int batched_phases(const BatchLayout& b, const float* X, int64_t n, int64
   uint64_t* thr = reinterpret_cast<uint64_t*>(w + b.off_thr);
   uint32_t* count = reinterpret_cast<uint32_t*>(w + b.off_count);
   uint64_t* cand = reinterpret_cast<uint64_t*>(w + b.off_cand);
-  int rc = launch_qnorm(Q, nq, (int)d, qnorm, st);
+  const bool l2 = metric == FX_METRIC_L2;
+  int rc = launch_qnorm(Q, nq, (int)d, qnorm, st, l2 ? 1 : 0);
   if (rc) return rc;
+  // fp32 error bound of |x|^2 + |q|^2 - 2 x.q relative to |x|^2 + |q|^2:
+  // 2 gamma_d for the three d-term sums + a few roundings, with 25 % slack
+  const float l2_eps = (float)((2.0 * (double)d + 8.0) * 5.9604644775390625e-08 * 1.25);
   hipError_t e = hipMemsetAsync(thr, 0xFF, (size_t)nq * 8, st);
   for (int ph = 0; ph < b.nphases && e == hipSuccess; ++ph) {
     e = hipMemsetAsync(count, 0, (size_t)nq * 4, st);
@@ -297,8 +302,13 @@ static int batched_phases(const BatchLayout& b, const float* X, int64_t n, int64
     a.count = count;
     a.cand = cand;
     a.cap = (int)b.cap;
+    a.l2_eps = l2_eps;
     rc = launch_batch(a, metric, st);
     if (rc) return rc;
+    if (l2) {  // approximate keys -> exact distances before any select
+      rc = launch_rescore(X, n, (int)d, row_base, Q, nq, count, cand, (int)b.cap, st);
+      if (rc) return rc;
+    }
     if (ph + 1 < b.nphases) {
       // the k-th composite of this sample bounds the global k-th from above
       rc = run_merge(b.merge, cand, nq, k, w + b.off_merge, nullptr, nullptr, st, thr);

@@ -61,7 +61,7 @@ struct BatchArgs {
   int d;
   int64_t row_base;
   const float* Q;         // [nq][d]
-  const float* qnorm;     // [nq] max(|q|, 1e-12) (cosine)
+  const float* qnorm;     // [nq] max(|q|, 1e-12) (cosine) / sum q^2 (L2)
   int64_t nq;
   const uint32_t* mask;
   int64_t tile_start, tile_stride, num_tiles;  // which 128-row tiles to scan
@@ -69,9 +69,16 @@ struct BatchArgs {
   uint32_t* count;        // [nq] appends (may exceed cap: overflow)
   uint64_t* cand;         // [nq][cap]
   int cap;
+  float l2_eps;           // L2: relative error bound of |x|^2+|q|^2-2x.q in fp32
 };
 int launch_batch(const BatchArgs& a, int metric, hipStream_t stream);
-int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stream);
+// mode 0: max(|q|, 1e-12) (cosine); mode 1: sum q^2 (L2 expansion)
+int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stream,
+                 int mode = 0);
+// L2 batches: replace each candidate's approximate key by its exact distance
+int launch_rescore(const float* X, int64_t n, int d, int64_t row_base, const float* Q,
+                   int64_t nq, const uint32_t* count, uint64_t* cand, int cap,
+                   hipStream_t stream);
 int batch_tile_rows();
 int launch_encode(const float* dist, const int64_t* row, int64_t count, uint64_t* out,
                   hipStream_t stream);

@@ -147,7 +147,7 @@ __global__ void __launch_bounds__(kThreads, kWaves * kBlocksPerCU / 4) batch_ker
 #pragma unroll
       for (int g = 0; g < kBK / 8; ++g) {
         const f32x4 av = ld4(xs + 8 * g);
-        if constexpr (METRIC == 2) {
+        if constexpr (METRIC != 1) {
           sumsq = fmaf(av[0], av[0], sumsq);
           sumsq = fmaf(av[1], av[1], sumsq);
           sumsq = fmaf(av[2], av[2], sumsq);
@@ -169,6 +169,9 @@ __global__ void __launch_bounds__(kThreads, kWaves * kBlocksPerCU / 4) batch_ker
     if constexpr (METRIC == 2) {
       sumsq += __shfl_xor(sumsq, 32);
       if (h == 0 && qtile0 == 0) sh->rownorm[rg * 32 + l32] = fmaxf(sqrtf(sumsq), 1e-12f);
+    } else if constexpr (METRIC == 0) {
+      sumsq += __shfl_xor(sumsq, 32);
+      if (h == 0 && qtile0 == 0) sh->rownorm[rg * 32 + l32] = sumsq;  // |x|^2
     }
     __syncthreads();
 #pragma unroll
@@ -178,18 +181,33 @@ __global__ void __launch_bounds__(kThreads, kWaves * kBlocksPerCU / 4) batch_ker
       bool ok = row < a.n;
       if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
       float nx = 1.f;
-      if constexpr (METRIC == 2) nx = sh->rownorm[lr];
+      if constexpr (METRIC != 1) nx = sh->rownorm[lr];
 #pragma unroll
       for (int qt = 0; qt < kQTiles; ++qt) {
         const float dot = acc[qt][r];
         float dist;
-        if constexpr (METRIC == 1) {
-          dist = -dot;
+        bool pass;
+        uint64_t comp;
+        if constexpr (METRIC == 0) {
+          // |x-q|^2 by expansion: an approximation whose fp32 error is at most
+          // l2_eps * (|x|^2 + |q|^2); a row passes if its lower bound can be
+          // within the threshold, and is rescored exactly (rescore_kernel)
+          // before any threshold or result is taken from it.
+          const float s2 = nx + qn[qt];
+          const float d2 = fmaxf(s2 - 2.f * dot, 0.f);
+          const float lo = fmaxf(d2 - a.l2_eps * s2, 0.f);
+          comp = make_comp(d2, (uint32_t)(a.row_base + row));
+          pass = order_key(sqrtf(lo)) <= (uint32_t)(thr[qt] >> 32);
         } else {
-          dist = 0.5f - 0.5f * (dot / (nx * qn[qt]));
+          if constexpr (METRIC == 1) {
+            dist = -dot;
+          } else {
+            dist = 0.5f - 0.5f * (dot / (nx * qn[qt]));
+          }
+          comp = make_comp(dist, (uint32_t)(a.row_base + row));
+          pass = comp <= thr[qt];
         }
-        const uint64_t comp = make_comp(dist, (uint32_t)(a.row_base + row));
-        if (ok && comp <= thr[qt]) {
+        if (ok && pass) {
           const int64_t gq = q0 + (qtile0 + qt) * 32 + l32;
           const uint32_t pos = atomicAdd(&a.count[gq], 1u);
           if (pos < (uint32_t)a.cap) a.cand[gq * a.cap + pos] = comp;
@@ -202,12 +220,16 @@ __global__ void __launch_bounds__(kThreads, kWaves * kBlocksPerCU / 4) batch_ker
 int launch_batch(const BatchArgs& a, int metric, hipStream_t stream) {
   if (a.num_tiles <= 0) return FX_OK;
   const size_t smem = sizeof(BatchShared);
-  const void* fn = metric == FX_METRIC_COS ? (const void*)batch_kernel<2> : (const void*)batch_kernel<1>;
+  const void* fn = metric == FX_METRIC_COS ? (const void*)batch_kernel<2>
+                   : metric == FX_METRIC_IP ? (const void*)batch_kernel<1>
+                                            : (const void*)batch_kernel<0>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)batch_kernel<2>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     (void)hipFuncSetAttribute((const void*)batch_kernel<1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    (void)hipFuncSetAttribute((const void*)batch_kernel<0>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
@@ -239,8 +261,10 @@ int launch_batch(const BatchArgs& a, int metric, hipStream_t stream) {
 
 int batch_tile_rows() { return kBM; }
 
-// cosine: max(||q||, 1e-12) per query (F.normalize eps, coder.py:43-44)
-__global__ void qnorm_kernel(const float* __restrict__ Q, int64_t nq, int d, float* __restrict__ out) {
+// cosine: max(||q||, 1e-12) per query (F.normalize eps, coder.py:43-44);
+// L2 (mode 1): sum of squares for the expansion
+__global__ void qnorm_kernel(const float* __restrict__ Q, int64_t nq, int d, float* __restrict__ out,
+                             int mode) {
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (q >= nq) return;
@@ -248,13 +272,71 @@ __global__ void qnorm_kernel(const float* __restrict__ Q, int64_t nq, int d, flo
   for (int i = lane; i < d; i += 64) s = fmaf(Q[q * d + i], Q[q * d + i], s);
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
-  if (lane == 0) out[q] = fmaxf(sqrtf(s), 1e-12f);
+  if (lane == 0) out[q] = mode == 1 ? s : fmaxf(sqrtf(s), 1e-12f);
 }
 
-int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stream) {
+int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stream, int mode) {
   hipLaunchKernelGGL(qnorm_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, stream, Q, nq, d,
-                     out);
+                     out, mode);
   return check_launch("qnorm_kernel");
+}
+
+// Exact L2 of each appended candidate: 16 lanes per candidate (4 per wave),
+// 16-B loads of the row and the query, the scan's direct sum of (x - q)^2 in
+// the scan's lane/slot order and reduction (the same f32 distance as the
+// single-query path), sqrt; the key is replaced in place (row unchanged).
+// Every lane of a wave runs the same number of iterations (sum16 is a
+// cross-lane reduction).
+__global__ void __launch_bounds__(256) rescore_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                      int64_t row_base,
+                                                      const float* __restrict__ Q,
+                                                      const uint32_t* __restrict__ count,
+                                                      uint64_t* __restrict__ cand, int cap) {
+  const int64_t q = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int grp = lane >> 4, jl = lane & 15;
+  const uint32_t cnt = count[q] < (uint32_t)cap ? count[q] : (uint32_t)cap;
+  const float* qv = Q + q * (int64_t)d;
+  for (int64_t i0 = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 6) * 4; i0 < cnt;
+       i0 += (int64_t)gridDim.x * 16) {  // wave-uniform trip count
+    const int64_t i = i0 + grp;
+    uint64_t* slot = cand + q * (int64_t)cap + (i < cnt ? i : i0);
+    const uint64_t c = i < cnt ? *slot : kEmpty;
+    const int64_t row = (int64_t)(c & 0xffffffffull) - row_base;
+    const bool live = c != kEmpty && row >= 0 && row < n;
+    float acc = 0.f;
+    if (live) {
+      const float* xr = X + row * (int64_t)d;
+      for (int k = jl * 4; k < d; k += 64) {
+        const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + k);
+        const f32x4 yv = *reinterpret_cast<const f32x4*>(qv + k);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float df = xv[t] - yv[t];
+          acc = fmaf(df, df, acc);
+        }
+      }
+    }
+    acc = sum16(acc);  // the scan's reduction: bit-identical distances
+    if (live && jl == 0) *slot = make_comp(sqrtf(acc), (uint32_t)(c & 0xffffffffull));
+  }
+}
+
+int launch_rescore(const float* X, int64_t n, int d, int64_t row_base, const float* Q, int64_t nq,
+                   const uint32_t* count, uint64_t* cand, int cap, hipStream_t stream) {
+  int cus = 0;
+  int rc = device_cus(&cus);
+  if (rc) return rc;
+  int64_t bx = ((int64_t)cap + 15) / 16;
+  if (bx > cus) bx = cus;
+  for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
+    const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
+    hipLaunchKernelGGL(rescore_kernel, dim3((unsigned)bx, (unsigned)qn), dim3(256), 0, stream, X,
+                       n, d, row_base, Q + q0 * d, count + q0, cand + q0 * (int64_t)cap, cap);
+    rc = check_launch("rescore_kernel");
+    if (rc) return rc;
+  }
+  return FX_OK;
 }
 
 }  // namespace fx

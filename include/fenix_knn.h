@@ -104,8 +104,9 @@ int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
  * fx_knn_scan launches the scan kernels (candidates into ws); fx_knn_reduce
  * launches the merge that turns them into out_dist / out_row.  Both must be
  * given the same arguments.
- * Batched queries (nq >= 8, float32, inner product / cosine) take the MFMA
- * path: fx_knn_scan runs the sampled-threshold GEMM phases and fx_knn_reduce
+ * Batched queries (nq >= 8, float32, any metric; L2 through the expansion
+ * with exact rescoring of the candidates) take the MFMA path: fx_knn_scan runs
+ * the sampled-threshold GEMM phases and fx_knn_reduce
  * synchronises the stream once to recompute any query whose candidates
  * overflowed (exact single-query scan), so it is not graph-capturable.
  */

@@ -310,7 +310,7 @@ def test_error_paths(eng):
     (200_000, 96, 300, 1000),   # two query tiles, k = 1000
     (70_001, 36, 9, 33),        # ragged tail tile, d not a multiple of 32
 ])
-@pytest.mark.parametrize("metric", ["inner_product", "cosine"])
+@pytest.mark.parametrize("metric", ["l2", "inner_product", "cosine"])
 def test_batched_mfma_parity(eng, n, d, nq, k, metric):
     x = gpu_fill(eng, n, d, seed=n % 97)
     xh = O.fill_normal(n, d, n % 97)
@@ -327,7 +327,7 @@ def test_batched_masked_and_clustered(eng):
     q = O.fill_normal(nq, d, seed=4, cluster=0)
     q[:8] = xh[[5, 1500, 77_777, 119_999, 2, 3, 4, 60_000]]  # queries inside clusters
     mask = np.random.RandomState(7).rand(n) < 0.3
-    for metric in ("inner_product", "cosine"):
+    for metric in ("l2", "inner_product", "cosine"):
         gd, gr = gpu_search(eng, x, q, metric, k, mask=mask, row_base=17)
         od, orow = O.knn(xh, q, metric, k, mask=mask, row_base=17)
         check_topk(gd, gr, od, orow, xh, q, metric)
@@ -340,6 +340,9 @@ def test_batched_overflow_fallback(eng, monkeypatch):
     x = gpu_fill(eng, n, d, seed=9)
     xh = O.fill_normal(n, d, 9)
     q = O.fill_normal(nq, d, seed=10)
+    ld, lr = gpu_search(eng, x, q, "l2", k)  # L2 batches: expansion filter + rescoring
+    old, olr = O.knn(xh, q, "l2", k)
+    check_topk(ld, lr, old, olr, xh, q, "l2")
     base_d, base_r = gpu_search(eng, x, q, "cosine", k)
     monkeypatch.setenv("FX_BATCH_FORCE_FALLBACK", "1")
     fd, fr = gpu_search(eng, x, q, "cosine", k)
@@ -353,18 +356,26 @@ def test_batched_overflow_fallback(eng, monkeypatch):
 
 
 def test_batched_equals_unbatched(eng, monkeypatch):
-    """The MFMA path and the per-query scan agree (ids; distances to f32 rounding)."""
+    """The MFMA path and the per-query scan agree (ids; distances to f32
+    rounding — and bit for bit for L2, whose candidates are rescored with the
+    scan's own summation order)."""
     n, d, nq, k = 100_000, 768, 24, 100
     x = gpu_fill(eng, n, d, seed=11)
     q = O.fill_normal(nq, d, seed=12)
-    bd, br = gpu_search(eng, x, q, "cosine", k)
-    monkeypatch.setenv("FX_BATCH", "0")
-    sd, sr = gpu_search(eng, x, q, "cosine", k)
     xh = O.fill_normal(n, d, 11)
-    od, orow = O.knn(xh, q, "cosine", k)
-    check_topk(bd, br, od, orow, xh, q, "cosine")
-    check_topk(sd, sr, od, orow, xh, q, "cosine")
-    assert np.max(np.abs(bd - sd)) <= 1e-6
+    for metric in ("cosine", "l2"):
+        monkeypatch.delenv("FX_BATCH", raising=False)
+        bd, br = gpu_search(eng, x, q, metric, k)
+        monkeypatch.setenv("FX_BATCH", "0")
+        sd, sr = gpu_search(eng, x, q, metric, k)
+        od, orow = O.knn(xh, q, metric, k)
+        check_topk(bd, br, od, orow, xh, q, metric)
+        check_topk(sd, sr, od, orow, xh, q, metric)
+        if metric == "l2":
+            np.testing.assert_array_equal(br, sr)
+            np.testing.assert_array_equal(bd, sd)
+        else:
+            assert np.max(np.abs(bd - sd)) <= 1e-6
 
 
 # ---------------------------------------------------------------- row lists

@@ -29,6 +29,8 @@ for step in "$@"; do
     benchq8) run benchq8 600 python -u bench.py --dtype qu8 --steps 10 --warmup 2 ;;
     benchq8all) run benchq8ip 300 python -u bench.py --dtype qu8 --steps 10 --warmup 2 --metric inner_product --no-cpu-baseline && run benchq8cos 300 python -u bench.py --dtype qu8 --steps 10 --warmup 2 --metric cosine --no-cpu-baseline ;;
     profq8) run profq8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profq8 -o run --output-format csv -- python3 -u bench.py --dtype qu8 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    testbatch) run pytest_batch 900 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k batch -p no:cacheprovider ;;
+    bench3l2) run bench3l2 900 python -u bench.py --nq 256 --metric l2 --steps 5 --warmup 1 --no-cpu-baseline ;;
     testk) run pytest_kernels 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_fullsize.py -m gpu -q -x -p no:cacheprovider ;;
     testsall) run pytest_gpu 1500 python -u -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python -u bench.py ;;
