@@ -34,7 +34,13 @@ namespace fx {
 #endif
 constexpr int kBM = 128;        // rows per block tile
 constexpr int kBQ = FX_BATCH_BQ;  // queries per block
-constexpr int kBK = 32;         // K chunk
+#ifndef FX_BATCH_BK
+#define FX_BATCH_BK 32
+#endif
+#ifndef FX_BATCH_BPC
+#define FX_BATCH_BPC (FX_BATCH_BQ == 256 ? 1 : 2)  // blocks per CU the LDS allows
+#endif
+constexpr int kBK = FX_BATCH_BK;  // K chunk
 constexpr int kLds = kBK + 4;   // padded LDS row (floats)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -54,21 +60,22 @@ __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<
 constexpr int kWaves = FX_BATCH_WAVES;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kQTiles = (kBQ / 32) * 4 / kWaves;  // 32-query MFMA tiles per wave
-constexpr int kBlocksPerCU = kBQ == 256 ? 1 : 2;
+constexpr int kBlocksPerCU = FX_BATCH_BPC;
+constexpr int kC4 = kBK / 4;  // 16-B pieces per row per chunk
 
 // Stage one K chunk (columns [k0, k0+32)) of X rows [r0, r0+128) and of the
 // query tile into registers (16-B pieces; 1024 of X, 2048 of Q per chunk).
 struct Prefetch {
-  f32x4 x[kBM * 8 / kThreads];
-  f32x4 q[kBQ * 8 / kThreads];
+  f32x4 x[kBM * kC4 / kThreads];
+  f32x4 q[kBQ * kC4 / kThreads];
 };
 
 __device__ __forceinline__ void prefetch_chunk(Prefetch& p, const BatchArgs& a, int64_t r0,
                                                int64_t q0, int k0, int tid) {
 #pragma unroll
-  for (int i = 0; i < kBM * 8 / kThreads; ++i) {
-    const int idx = i * kThreads + tid;  // row = idx/8, col4 = idx%8
-    const int row = idx >> 3, c4 = idx & 7;
+  for (int i = 0; i < kBM * kC4 / kThreads; ++i) {
+    const int idx = i * kThreads + tid;  // row = idx/kC4, col4 = idx%kC4
+    const int row = idx / kC4, c4 = idx % kC4;
     const int64_t gr = r0 + row;
     const int k = k0 + c4 * 4;
     if (gr < a.n && k < a.d) {
@@ -79,9 +86,9 @@ __device__ __forceinline__ void prefetch_chunk(Prefetch& p, const BatchArgs& a, 
     }
   }
 #pragma unroll
-  for (int i = 0; i < kBQ * 8 / kThreads; ++i) {
-    const int idx = i * kThreads + tid;  // query = idx/8, col4 = idx%8
-    const int qq = idx >> 3, c4 = idx & 7;
+  for (int i = 0; i < kBQ * kC4 / kThreads; ++i) {
+    const int idx = i * kThreads + tid;  // query = idx/kC4, col4 = idx%kC4
+    const int qq = idx / kC4, c4 = idx % kC4;
     const int64_t gq = q0 + qq;
     const int k = k0 + c4 * 4;
     p.q[i] = (gq < a.nq && k < a.d) ? ld4(a.Q + gq * (int64_t)a.d + k) : f32x4(0.f);
@@ -90,14 +97,14 @@ __device__ __forceinline__ void prefetch_chunk(Prefetch& p, const BatchArgs& a, 
 
 __device__ __forceinline__ void store_chunk(const Prefetch& p, BatchShared* sh, int buf, int tid) {
 #pragma unroll
-  for (int i = 0; i < kBM * 8 / kThreads; ++i) {
+  for (int i = 0; i < kBM * kC4 / kThreads; ++i) {
     const int idx = i * kThreads + tid;
-    *reinterpret_cast<f32x4*>(&sh->xs[buf][(idx >> 3) * kLds + (idx & 7) * 4]) = p.x[i];
+    *reinterpret_cast<f32x4*>(&sh->xs[buf][(idx / kC4) * kLds + (idx % kC4) * 4]) = p.x[i];
   }
 #pragma unroll
-  for (int i = 0; i < kBQ * 8 / kThreads; ++i) {
+  for (int i = 0; i < kBQ * kC4 / kThreads; ++i) {
     const int idx = i * kThreads + tid;
-    *reinterpret_cast<f32x4*>(&sh->qs[buf][(idx >> 3) * kLds + (idx & 7) * 4]) = p.q[i];
+    *reinterpret_cast<f32x4*>(&sh->qs[buf][(idx / kC4) * kLds + (idx % kC4) * 4]) = p.q[i];
   }
 }
 
