@@ -328,7 +328,7 @@ using namespace fx;
 
 extern "C" {
 
-int fx_version(void) { return 100; }
+int fx_version(void) { return 101; }
 
 const char* fx_last_error(void) { return g_err; }
 

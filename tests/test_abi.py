@@ -40,7 +40,7 @@ def test_library_is_gfx950():
 
 def test_version_and_limits():
     lib = _lib.load()
-    assert lib.fx_version() == 100
+    assert lib.fx_version() == 101  # 1.1: coded index, row lists, _ex, large k, RCCL
     assert _lib.max_k() == 1024
 
 
