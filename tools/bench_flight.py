@@ -64,6 +64,7 @@ def main() -> None:
     p.add_argument("--dtype", default="f32", choices=["f32", "f16"])
     p.add_argument("--batch", type=int, default=1000)
     p.add_argument("--reps", type=int, default=30)
+    p.add_argument("--clients", type=int, default=1, help="concurrent client processes")
     p.add_argument("--client", action="store_true")
     p.add_argument("--port", type=int, default=0)
     a = p.parse_args()
@@ -102,13 +103,20 @@ def main() -> None:
     cmd = [sys.executable, os.path.abspath(__file__), "--client", "--port", str(port),
            "--d", str(a.d), "--k", str(a.k), "--metric", a.metric, "--dtype", a.dtype,
            "--reps", str(a.reps)]
-    proc = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    t_all = time.perf_counter()
+    procs = [subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for _ in range(a.clients)]
+    outs = [p_.communicate(timeout=600) for p_ in procs]
+    wall = time.perf_counter() - t_all
     server.shutdown()
-    if proc.returncode != 0:
-        print(proc.stderr, file=sys.stderr)
-        raise SystemExit(proc.returncode)
-    res = json.loads(proc.stdout.strip().splitlines()[-1])
-    lat = np.array(res["lat_ms"])
+    results = []
+    for p_, (out, err) in zip(procs, outs):
+        if p_.returncode != 0:
+            print(err, file=sys.stderr)
+            raise SystemExit(p_.returncode)
+        results.append(json.loads(out.strip().splitlines()[-1]))
+    res = results[0]
+    lat = np.concatenate([np.array(r["lat_ms"]) for r in results])
     med = float(np.median(lat))
     print(json.dumps({
         "workload": f"{a.n}x{a.d} {a.dtype} {a.metric} k={a.k} via Flight.search "
@@ -120,6 +128,10 @@ def main() -> None:
         "make_table_s": t_put,
         "reps": a.reps,
         "client_imported_torch": res["torch_imported"],
+        "clients": a.clients,
+        "aggregate_searches_per_s": a.clients * a.reps / sum(
+            np.sum(r["lat_ms"]) / 1e3 / a.clients for r in results) if a.clients > 1 else None,
+        "wall_s_incl_client_start": wall,
     }), flush=True)
 
 
