@@ -121,12 +121,21 @@ static constexpr int64_t kBatchMinQ = 8;
 static constexpr int64_t kListLen = 4096;  // candidate buffer viewed as lists
 
 struct BatchLayout {
-  int64_t cap = 0, tiles = 0;
+  int64_t cap = 0, tiles = 0, nq_pad = 0;
   int nphases = 0;
+  bool filter = false;  // fp16-MFMA filter + exact rescoring (knn_filter.hip)
+  int dq = 0;
   int64_t start[16], stride[16], num[16];
   MergePlan merge;
-  size_t off_qnorm, off_thr, off_count, off_cand, off_merge, total;
+  size_t off_qnorm, off_thr, off_count, off_cand, off_merge, off_cand_ub, off_qh, off_qinfo,
+      total;
 };
+
+// FX_BATCH_FILTER=0 selects the fp32-MFMA batch kernel (knn_batch.hip)
+static bool use_filter() {
+  const char* env = getenv("FX_BATCH_FILTER");
+  return env == nullptr || atoi(env) != 0;
+}
 
 static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool aligned) {
   if (const char* env = getenv("FX_BATCH")) {
@@ -135,8 +144,9 @@ static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool align
   return nq >= kBatchMinQ && dtype == FX_DTYPE_F32 && d % 4 == 0 && aligned;
 }
 
-static int plan_batched(int64_t n, int64_t nq, int64_t k, BatchLayout* b) {
-  const int64_t tr = batch_tile_rows();
+static int plan_batched(int64_t n, int64_t d, int64_t nq, int64_t k, BatchLayout* b) {
+  b->filter = use_filter();
+  const int64_t tr = b->filter ? filter_tile_rows() : batch_tile_rows();
   b->cap = 64 * k > 16384 ? 64 * k : 16384;
   if (const char* env = getenv("FX_BATCH_CAP")) {  // test knob: small buffers
     const int64_t c = atoll(env);
@@ -174,11 +184,21 @@ static int plan_batched(int64_t n, int64_t nq, int64_t k, BatchLayout* b) {
   b->off_thr = off;
   off += align256((size_t)nq * 8);
   b->off_count = off;
-  off += align256((size_t)nq * 4);
+  off += align256((size_t)nq * 4 * kCountStride);
   b->off_cand = off;
   off += align256((size_t)nq * b->cap * 8);
   b->off_merge = off;
   off += align256(b->merge.ws_bytes);
+  if (b->filter) {
+    b->dq = filter_dq((int)d);
+    b->nq_pad = (nq + filter_query_pad() - 1) / filter_query_pad() * filter_query_pad();
+    b->off_cand_ub = off;
+    off += align256((size_t)nq * b->cap * 8);
+    b->off_qh = off;
+    off += align256((size_t)b->nq_pad * b->dq * 2);
+    b->off_qinfo = off;
+    off += align256((size_t)nq * 16);
+  }
   b->total = off;
   return FX_OK;
 }
@@ -228,7 +248,7 @@ static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, i
   int rc = plan_single(n, d, dtype, 1, k, metric, aligned, s);
   if (rc) return rc;
   const size_t single_total = s->total;
-  rc = plan_batched(n, nq, k, &s->batch);
+  rc = plan_batched(n, d, nq, k, &s->batch);
   if (rc) return rc;
   s->batched = true;
   s->single_off = s->batch.total;
@@ -268,6 +288,71 @@ static int single_search(const void* corpus, int dtype, int64_t n, int64_t d, in
                    out_dist, out_row, st);
 }
 
+// fp16 filter phases (knn_filter.hip).  Sampling phases append the UPPER
+// bound of every row whose lower bound reaches the threshold; the k-th upper
+// bound of any row subset bounds the global k-th distance from above, so it is
+// the next phase's threshold.  The final phase (every row) appends lower and
+// upper bounds; the k-th upper bound among its candidates is a tighter
+// threshold, and only candidates whose lower bound reaches it are rescored
+// exactly (the rest are dropped unread).  fx_knn_reduce then selects the top k
+// of the exact keys and recomputes overflowing queries.
+static int filter_phases(const BatchLayout& b, const float* X, int64_t n, int64_t d,
+                         int64_t row_base, const float* Q, int64_t nq, int metric, int64_t k,
+                         const uint32_t* mask, char* w, hipStream_t st) {
+  float* qnorm = reinterpret_cast<float*>(w + b.off_qnorm);
+  uint64_t* thr = reinterpret_cast<uint64_t*>(w + b.off_thr);
+  uint32_t* count = reinterpret_cast<uint32_t*>(w + b.off_count);
+  uint64_t* cand = reinterpret_cast<uint64_t*>(w + b.off_cand);
+  uint64_t* cand_ub = reinterpret_cast<uint64_t*>(w + b.off_cand_ub);
+  uint16_t* qh = reinterpret_cast<uint16_t*>(w + b.off_qh);
+  float* qinfo = reinterpret_cast<float*>(w + b.off_qinfo);
+  int rc = launch_qprep(Q, nq, b.nq_pad, (int)d, b.dq, metric, qh, qinfo, st);
+  if (rc) return rc;
+  if (metric == FX_METRIC_COS) {  // the scan's max(|q|, 1e-12) for the rescoring
+    rc = launch_qnorm(Q, nq, (int)d, qnorm, st, 0);
+    if (rc) return rc;
+  }
+  hipError_t e = hipMemsetAsync(thr, 0xFF, (size_t)nq * 8, st);
+  for (int ph = 0; ph < b.nphases && e == hipSuccess; ++ph) {
+    const bool last = ph + 1 == b.nphases;
+    e = hipMemsetAsync(count, 0, (size_t)nq * 4 * kCountStride, st);
+    if (e == hipSuccess) e = hipMemsetAsync(cand, 0xFF, (size_t)nq * b.cap * 8, st);
+    if (e == hipSuccess && last) e = hipMemsetAsync(cand_ub, 0xFF, (size_t)nq * b.cap * 8, st);
+    if (e != hipSuccess) break;
+    FilterArgs a = {};
+    a.X = X;
+    a.n = n;
+    a.d = (int)d;
+    a.row_base = row_base;
+    a.Qh = qh;
+    a.dq = b.dq;
+    a.qinfo = qinfo;
+    a.nq = nq;
+    a.mask = mask;
+    a.tile_start = b.start[ph];
+    a.tile_stride = b.stride[ph];
+    a.num_tiles = b.num[ph];
+    a.thr = thr;
+    a.count = count;
+    a.cand = cand;
+    a.cand_ub = last ? cand_ub : nullptr;
+    a.cap = (int)b.cap;
+    if (const char* dg = getenv("FX_FILTER_DIAG")) a.diag = atoi(dg);
+    rc = launch_filter(a, metric, st);
+    if (rc) return rc;
+    // the k-th upper bound of this phase's candidates: next threshold
+    rc = run_merge(b.merge, last ? cand_ub : cand, nq, k, w + b.off_merge, nullptr, nullptr, st,
+                   thr);
+    if (rc) return rc;
+  }
+  if (e != hipSuccess) {
+    set_error("batched memset: %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  return launch_rescore(X, n, (int)d, row_base, Q, qnorm, nq, count, cand, (int)b.cap, metric,
+                        thr, st);
+}
+
 static int batched_phases(const BatchLayout& b, const float* X, int64_t n, int64_t d,
                           int64_t row_base, const float* Q, int64_t nq, int metric, int64_t k,
                           const uint32_t* mask, char* w, hipStream_t st) {
@@ -283,7 +368,7 @@ static int batched_phases(const BatchLayout& b, const float* X, int64_t n, int64
   const float l2_eps = (float)((2.0 * (double)d + 8.0) * 5.9604644775390625e-08 * 1.25);
   hipError_t e = hipMemsetAsync(thr, 0xFF, (size_t)nq * 8, st);
   for (int ph = 0; ph < b.nphases && e == hipSuccess; ++ph) {
-    e = hipMemsetAsync(count, 0, (size_t)nq * 4, st);
+    e = hipMemsetAsync(count, 0, (size_t)nq * 4 * kCountStride, st);
     if (e == hipSuccess) e = hipMemsetAsync(cand, 0xFF, (size_t)nq * b.cap * 8, st);
     if (e != hipSuccess) break;
     BatchArgs a = {};
@@ -306,7 +391,8 @@ static int batched_phases(const BatchLayout& b, const float* X, int64_t n, int64
     rc = launch_batch(a, metric, st);
     if (rc) return rc;
     if (l2) {  // approximate keys -> exact distances before any select
-      rc = launch_rescore(X, n, (int)d, row_base, Q, nq, count, cand, (int)b.cap, st);
+      rc = launch_rescore(X, n, (int)d, row_base, Q, nullptr, nq, count, cand, (int)b.cap,
+                          FX_METRIC_L2, nullptr, st);
       if (rc) return rc;
     }
     if (ph + 1 < b.nphases) {
@@ -410,6 +496,10 @@ int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (s.batched) {
+    if (s.batch.filter) {
+      return filter_phases(s.batch, reinterpret_cast<const float*>(corpus), n, d, row_base,
+                           queries, nq, metric, k, mask, reinterpret_cast<char*>(ws), st);
+    }
     return batched_phases(s.batch, reinterpret_cast<const float*>(corpus), n, d, row_base,
                           queries, nq, metric, k, mask, reinterpret_cast<char*>(ws), st);
   }
@@ -476,8 +566,8 @@ int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
   if (rc) return rc;
   // queries whose candidates overflowed `cap`: recompute exactly, one by one
   std::vector<uint32_t> counts((size_t)nq);
-  hipError_t e = hipMemcpyAsync(counts.data(), w + b.off_count, (size_t)nq * 4,
-                                hipMemcpyDeviceToHost, st);
+  hipError_t e = hipMemcpy2DAsync(counts.data(), 4, w + b.off_count, 4 * kCountStride, 4,
+                                  (size_t)nq, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) {
     set_error("batched overflow check: %s", hipGetErrorString(e));

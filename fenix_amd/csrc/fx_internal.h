@@ -8,6 +8,9 @@ namespace fx {
 
 constexpr int kModeTopk = 0;
 constexpr int kModeDist = 1;
+// Per-query append counters of the batched kernels sit 128 B apart: every
+// counter in its own cache line, so the L2 channels serialise fewer atomics.
+constexpr int kCountStride = 32;
 
 struct ScanArgs {
   const void* X;          // [n][d] corpus shard
@@ -66,7 +69,7 @@ struct BatchArgs {
   const uint32_t* mask;
   int64_t tile_start, tile_stride, num_tiles;  // which 128-row tiles to scan
   const uint64_t* thr;    // [nq] append rows whose composite <= thr
-  uint32_t* count;        // [nq] appends (may exceed cap: overflow)
+  uint32_t* count;        // [nq * kCountStride] appends (may exceed cap: overflow)
   uint64_t* cand;         // [nq][cap]
   int cap;
   float l2_eps;           // L2: relative error bound of |x|^2+|q|^2-2x.q in fp32
@@ -75,10 +78,41 @@ int launch_batch(const BatchArgs& a, int metric, hipStream_t stream);
 // mode 0: max(|q|, 1e-12) (cosine); mode 1: sum q^2 (L2 expansion)
 int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stream,
                  int mode = 0);
-// L2 batches: replace each candidate's approximate key by its exact distance
+// Replace each candidate's key by its exact distance (the single-query scan's
+// summation order: bit-identical).  thr (optional): candidates whose key is
+// above the query's thr key are dropped (kEmpty) without being read.
+// qnorm: cosine only, max(|q|, 1e-12) as the scan computes it.
 int launch_rescore(const float* X, int64_t n, int d, int64_t row_base, const float* Q,
-                   int64_t nq, const uint32_t* count, uint64_t* cand, int cap,
-                   hipStream_t stream);
+                   const float* qnorm, int64_t nq, const uint32_t* count, uint64_t* cand,
+                   int cap, int metric, const uint64_t* thr, hipStream_t stream);
+
+// Batched filter on the fp16 matrix cores (knn_filter.hip): appends every
+// (row, query) whose rigorous lower bound reaches the query's threshold.
+struct FilterArgs {
+  const float* X;         // [n][d] f32 corpus shard
+  int64_t n;
+  int d;
+  int64_t row_base;
+  const uint16_t* Qh;     // [nq_pad][dq] fp16 queries, scaled by a power of two
+  int dq;
+  const float* qinfo;     // [nq][4] {1/scale, norm term, A, B}
+  int64_t nq;
+  const uint32_t* mask;
+  int64_t tile_start, tile_stride, num_tiles;  // which 256-row tiles to scan
+  const uint64_t* thr;    // [nq] append when order_key(lb) <= thr >> 32
+  uint32_t* count;        // [nq * kCountStride] appends (may exceed cap: overflow)
+  uint64_t* cand;         // [nq][cap] ub composites (cand_ub null) or lb composites
+  uint64_t* cand_ub;      // [nq][cap] ub composites, or null (sampling phases)
+  int cap;
+  int diag;               // FX_FILTER_DIAG (profiling only): 1 no appends, 2 no epilogue,
+                          // 4 no MFMA
+};
+int launch_filter(const FilterArgs& a, int metric, hipStream_t stream);
+int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
+                 uint16_t* Qh, float* qinfo, hipStream_t stream);
+int filter_tile_rows();
+int filter_query_pad();
+int filter_dq(int d);
 int batch_tile_rows();
 int launch_encode(const float* dist, const int64_t* row, int64_t count, uint64_t* out,
                   hipStream_t stream);

@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(kThreads, kWaves * kBlocksPerCU / 4) batch_ker
         }
         if (ok && pass) {
           const int64_t gq = q0 + (qtile0 + qt) * 32 + l32;
-          const uint32_t pos = atomicAdd(&a.count[gq], 1u);
+          const uint32_t pos = atomicAdd(&a.count[gq * kCountStride], 1u);
           if (pos < (uint32_t)a.cap) a.cand[gq * a.cap + pos] = comp;
         }
       }
@@ -252,7 +252,7 @@ int launch_batch(const BatchArgs& a, int metric, hipStream_t stream) {
     b.Q = a.Q + y0 * kBQ * (int64_t)a.d;
     b.qnorm = a.qnorm + y0 * kBQ;
     b.thr = a.thr + y0 * kBQ;
-    b.count = a.count + y0 * kBQ;
+    b.count = a.count + y0 * kBQ * kCountStride;
     b.cand = a.cand + y0 * kBQ * (int64_t)a.cap;
     b.nq = a.nq - y0 * kBQ;
     void* args[] = {(void*)&b};
@@ -288,21 +288,28 @@ int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stre
   return check_launch("qnorm_kernel");
 }
 
-// Exact L2 of each appended candidate: 16 lanes per candidate (4 per wave),
-// 16-B loads of the row and the query, the scan's direct sum of (x - q)^2 in
-// the scan's lane/slot order and reduction (the same f32 distance as the
-// single-query path), sqrt; the key is replaced in place (row unchanged).
-// Every lane of a wave runs the same number of iterations (sum16 is a
-// cross-lane reduction).
+// Exact distance of each appended candidate: 16 lanes per candidate (4 per
+// wave), 16-B loads of the row and the query, the scan's per-lane fmaf chain
+// over slots jl, jl+16, ... (knn_scan.hip tile_accumulate) and its sum16
+// reduction, then the scan's distance formula (tile_finish): the same f32
+// distance as the single-query path, bit for bit.  The key is replaced in
+// place (row unchanged).  With thr, a candidate whose (lower-bound) key is
+// above the query's threshold key is dropped unread.  Every lane of a wave
+// runs the same number of iterations (sum16 is a cross-lane reduction).
+template <int METRIC>
 __global__ void __launch_bounds__(256) rescore_kernel(const float* __restrict__ X, int64_t n, int d,
                                                       int64_t row_base,
                                                       const float* __restrict__ Q,
+                                                      const float* __restrict__ qnorm,
                                                       const uint32_t* __restrict__ count,
-                                                      uint64_t* __restrict__ cand, int cap) {
+                                                      uint64_t* __restrict__ cand, int cap,
+                                                      const uint64_t* __restrict__ thr) {
   const int64_t q = blockIdx.y;
   const int lane = threadIdx.x & 63;
   const int grp = lane >> 4, jl = lane & 15;
-  const uint32_t cnt = count[q] < (uint32_t)cap ? count[q] : (uint32_t)cap;
+  const uint32_t cq = count[q * kCountStride];
+  const uint32_t cnt = cq < (uint32_t)cap ? cq : (uint32_t)cap;
+  const uint32_t tkey = thr != nullptr ? (uint32_t)(thr[q] >> 32) : 0xffffffffu;
   const float* qv = Q + q * (int64_t)d;
   for (int64_t i0 = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 6) * 4; i0 < cnt;
        i0 += (int64_t)gridDim.x * 16) {  // wave-uniform trip count
@@ -310,8 +317,9 @@ __global__ void __launch_bounds__(256) rescore_kernel(const float* __restrict__ 
     uint64_t* slot = cand + q * (int64_t)cap + (i < cnt ? i : i0);
     const uint64_t c = i < cnt ? *slot : kEmpty;
     const int64_t row = (int64_t)(c & 0xffffffffull) - row_base;
-    const bool live = c != kEmpty && row >= 0 && row < n;
-    float acc = 0.f;
+    const bool keep = c != kEmpty && (uint32_t)(c >> 32) <= tkey;
+    const bool live = keep && row >= 0 && row < n;
+    float acc = 0.f, acc2 = 0.f;
     if (live) {
       const float* xr = X + row * (int64_t)d;
       for (int k = jl * 4; k < d; k += 64) {
@@ -319,18 +327,38 @@ __global__ void __launch_bounds__(256) rescore_kernel(const float* __restrict__ 
         const f32x4 yv = *reinterpret_cast<const f32x4*>(qv + k);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const float df = xv[t] - yv[t];
-          acc = fmaf(df, df, acc);
+          if constexpr (METRIC == 0) {
+            const float df = xv[t] - yv[t];
+            acc = fmaf(df, df, acc);
+          } else if constexpr (METRIC == 1) {
+            acc = fmaf(xv[t], yv[t], acc);
+          } else {
+            acc = fmaf(xv[t], yv[t], acc);
+            acc2 = fmaf(xv[t], xv[t], acc2);
+          }
         }
       }
     }
-    acc = sum16(acc);  // the scan's reduction: bit-identical distances
-    if (live && jl == 0) *slot = make_comp(sqrtf(acc), (uint32_t)(c & 0xffffffffull));
+    const float s1 = sum16(acc);  // the scan's reduction: bit-identical distances
+    float dist;
+    if constexpr (METRIC == 0) {
+      dist = sqrtf(s1);
+    } else if constexpr (METRIC == 1) {
+      dist = -s1;
+    } else {
+      const float s2 = sum16(acc2);
+      const float nx = fmaxf(sqrtf(s2), 1e-12f);
+      dist = 0.5f - 0.5f * (s1 / (nx * qnorm[q]));
+    }
+    if (jl == 0 && i < cnt && c != kEmpty) {
+      *slot = live ? make_comp(dist, (uint32_t)(c & 0xffffffffull)) : kEmpty;
+    }
   }
 }
 
-int launch_rescore(const float* X, int64_t n, int d, int64_t row_base, const float* Q, int64_t nq,
-                   const uint32_t* count, uint64_t* cand, int cap, hipStream_t stream) {
+int launch_rescore(const float* X, int64_t n, int d, int64_t row_base, const float* Q,
+                   const float* qnorm, int64_t nq, const uint32_t* count, uint64_t* cand,
+                   int cap, int metric, const uint64_t* thr, hipStream_t stream) {
   int cus = 0;
   int rc = device_cus(&cus);
   if (rc) return rc;
@@ -338,8 +366,19 @@ int launch_rescore(const float* X, int64_t n, int d, int64_t row_base, const flo
   if (bx > cus) bx = cus;
   for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
     const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
-    hipLaunchKernelGGL(rescore_kernel, dim3((unsigned)bx, (unsigned)qn), dim3(256), 0, stream, X,
-                       n, d, row_base, Q + q0 * d, count + q0, cand + q0 * (int64_t)cap, cap);
+    const dim3 grid((unsigned)bx, (unsigned)qn);
+    const uint64_t* t = thr != nullptr ? thr + q0 : nullptr;
+    const float* qnm = qnorm != nullptr ? qnorm + q0 : nullptr;
+    if (metric == FX_METRIC_COS) {
+      hipLaunchKernelGGL(rescore_kernel<2>, grid, dim3(256), 0, stream, X, n, d, row_base,
+                         Q + q0 * d, qnm, count + q0 * kCountStride, cand + q0 * (int64_t)cap, cap, t);
+    } else if (metric == FX_METRIC_IP) {
+      hipLaunchKernelGGL(rescore_kernel<1>, grid, dim3(256), 0, stream, X, n, d, row_base,
+                         Q + q0 * d, qnm, count + q0 * kCountStride, cand + q0 * (int64_t)cap, cap, t);
+    } else {
+      hipLaunchKernelGGL(rescore_kernel<0>, grid, dim3(256), 0, stream, X, n, d, row_base,
+                         Q + q0 * d, qnm, count + q0 * kCountStride, cand + q0 * (int64_t)cap, cap, t);
+    }
     rc = check_launch("rescore_kernel");
     if (rc) return rc;
   }

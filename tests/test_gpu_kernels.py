@@ -378,6 +378,60 @@ def test_batched_equals_unbatched(eng, monkeypatch):
             assert np.max(np.abs(bd - sd)) <= 1e-6
 
 
+@pytest.mark.parametrize("metric", METRICS)
+@pytest.mark.parametrize("n,d,nq,k", [(100_000, 768, 40, 100), (30_011, 100, 300, 7)])
+def test_batched_filter_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq, k):
+    """fp16-MFMA filter + exact rescoring == the single-query f32 scan, bit for
+    bit (rows and distances), and the fp32-MFMA batch kernel agrees on ids."""
+    x = gpu_fill(eng, n, d, seed=21)
+    q = O.fill_normal(nq, d, seed=22)
+    monkeypatch.delenv("FX_BATCH", raising=False)
+    monkeypatch.delenv("FX_BATCH_FILTER", raising=False)
+    fd, fr = gpu_search(eng, x, q, metric, k)
+    monkeypatch.setenv("FX_BATCH", "0")
+    sd, sr = gpu_search(eng, x, q, metric, k)
+    np.testing.assert_array_equal(fr, sr)
+    np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
+    monkeypatch.delenv("FX_BATCH")
+    monkeypatch.setenv("FX_BATCH_FILTER", "0")
+    md, mr = gpu_search(eng, x, q, metric, k)
+    xh = O.fill_normal(n, d, 21)
+    od, orow = O.knn(xh, q, metric, k)
+    check_topk(md, mr, od, orow, xh, q, metric)
+    check_topk(fd, fr, od, orow, xh, q, metric)
+
+
+@pytest.mark.parametrize("metric", METRICS)
+def test_batched_filter_extreme_rows_and_queries(eng, monkeypatch, metric):
+    """Rows the fp16 filter cannot bound (|x| >= 65504, inf, NaN) are forced
+    through; tiny-magnitude rows and queries scaled by 2^+-60 still bound
+    correctly: results equal the scan's bit for bit."""
+    n, d, k = 20_000, 64, 25
+    xh = O.fill_normal(n, d, 31)
+    rs = np.random.RandomState(5)
+    big = rs.choice(n, 40, replace=False)
+    xh[big[:10]] *= 1e5                    # beyond fp16 range
+    xh[big[10:20]] *= 1e-7                 # fp16 subnormal / flushed range
+    xh[big[20:25], 3] = np.inf
+    xh[big[25:30], 7] = np.nan
+    xh[big[30:35]] = 0.0
+    xh[big[35:40]] *= 3e4                  # just below fp16 max
+    x = torch.from_numpy(xh).to(eng.device)
+    q = O.fill_normal(16, d, seed=32)
+    q[0] *= 2.0 ** 60
+    q[1] *= 2.0 ** -60
+    q[2] = xh[big[0]]                      # a query out of fp16 range
+    q[3] = xh[big[12]]                     # a tiny query
+    q[4] = 0.0
+    monkeypatch.delenv("FX_BATCH", raising=False)
+    fd, fr = gpu_search(eng, x, q, metric, k)
+    monkeypatch.setenv("FX_BATCH", "0")
+    sd, sr = gpu_search(eng, x, q, metric, k)
+    np.testing.assert_array_equal(fr, sr)
+    np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
+
+
+
 # ---------------------------------------------------------------- row lists
 
 
