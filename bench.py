@@ -32,6 +32,7 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md chip table
 MFMA_F32_PEAK_TFS = 157.3  # dense fp32 matrix peak (v_mfma_f32_32x32x2_f32), same table
+MFMA_F16_PEAK_TFS = 2500.0  # dense fp16/bf16 matrix peak, same table
 
 METRIC = "vectors/sec + %HBM roofline, 10M×768 f32 L2 kNN k=100 at 1/2/4/8 GPU"
 
@@ -238,9 +239,12 @@ def main():
     scan_bytes = n * d * esize + nq * d * 4
     tag = f"{n}x{d}_{args.dtype}_{args.metric}_k{k}_q{nq}"
     traffic = pmc_traffic(tag)
-    # batched inner-product / cosine queries run on the fp32 matrix cores
-    mfma = nq >= 8 and args.dtype == "f32"
-    if mfma:
+    # batched queries (f32): by default the fp16-MFMA bound filter + exact
+    # rescoring (knn_filter.hip), one HBM-bound pass over the corpus; with
+    # FX_BATCH_FILTER=0 the fp32-MFMA kernel (knn_batch.hip), MFMA-bound
+    batched = nq >= 8 and args.dtype == "f32"
+    filt = batched and os.environ.get("FX_BATCH_FILTER", "1") != "0"
+    if batched and not filt:
         flops = 2.0 * n * nq * d
         roof = {
             "bound": "mfma",
@@ -254,17 +258,26 @@ def main():
         }
     else:
         achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
+        if filt:
+            kname = ("fx::filter_kernel (fp16-MFMA bound filter, all sample phases) "
+                     "+ exact rescoring of the candidates")
+        elif qu8:
+            kname = "fx::scan_kernel<uint8> (quint8 codes dequantised in registers) + merge"
+        else:
+            kname = "fx::scan_kernel (fused distance + per-wave top-k)"
         roof = {
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "traffic": traffic,
-            "kernel": "fx::scan_kernel<uint8> (quint8 codes dequantised in registers) + merge"
-            if qu8 else "fx::scan_kernel (fused distance + per-wave top-k)",
+            "kernel": kname,
             "kernel_ms": scan_ms,
             "bytes_per_launch": scan_bytes,
         }
+        if filt:  # the GEMM the filter evaluates, against the dense fp16 MFMA peak
+            roof["mfma_tflops"] = 2.0 * n * nq * d / (scan_ms * 1e-3) / 1e12
+            roof["mfma_peak_tflops"] = MFMA_F16_PEAK_TFS
     roof["frac"] = roof["achieved"] / roof["peak"]
 
     out = None

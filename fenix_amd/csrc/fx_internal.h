@@ -105,7 +105,7 @@ struct FilterArgs {
   uint64_t* cand_ub;      // [nq][cap] ub composites, or null (sampling phases)
   int cap;
   int diag;               // FX_FILTER_DIAG (profiling only): 1 no appends, 2 no epilogue,
-                          // 4 no MFMA
+                          // 4 no MFMA, 8 no query loads, 16 no LDS stores
 };
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream);
 int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,

@@ -26,34 +26,60 @@
 //     L2   e = A (|x|^2 + |q|^2) + B     on the squared distance (the scan's
 //          direct sum of (x - q)^2 is within 2 (d + 2) g of it; covered)
 //     cos  e = A + B / max(|x|, 1e-12)   on 0.5 - 0.5 cos
-//   Rows with a component of magnitude >= 65504 (fp16 overflow), a non-finite
-//   sum of squares, or a query with non-finite norm are forced through
-//   (lb = -inf, ub = NaN, i.e. above every number).
+//   A component of magnitude >= 65520 (rounds to an fp16 infinity, so the
+//   product comes out non-finite), a non-finite sum of squares or a query with
+//   a non-finite norm forces the pair through (lb = -inf, ub = NaN, i.e. above
+//   every number).  Components in [65504, 65520) round to 65504 within u.
 //
-// Tile: 128 corpus rows x 256 queries per 512-thread workgroup (8 waves: 2 row
-// groups x 4 query groups of 64; each wave holds 2 x 2 accumulators of
-// v_mfma_f32_32x32x16_f16, 64 registers, so two waves share a SIMD).  K chunks
-// of 64 elements: the f32 rows are loaded with non-temporal 16-B loads two
-// chunks ahead (64 KB in flight per CU), converted to fp16 on the way into a
-// double-buffered LDS tile (rows padded to 144 B: conflict-free ds_read_b128
-// fragments); the pre-scaled fp16 query tile (L2-resident, 393 KB for
-// 256 x 768) is staged alongside.  Per-row sums of squares and max |x| come
-// from the same registers.
+// Tile: 256 corpus rows x 256 queries per 512-thread workgroup, one per CU
+// (8 waves, 2 per SIMD: 4 row groups of 64 x 2 query groups of 128; each wave
+// holds 2 x 4 accumulators of v_mfma_f32_32x32x16_f16).  K chunks of 32: the
+// f32 rows stream in through buffer loads (non-temporal) two chunks ahead,
+// are converted to fp16 on their way into a double-buffered LDS tile (rows
+// padded by 16 B: conflict-free ds_read_b128 fragments); the pre-scaled fp16
+// query tile (L2-resident, 393 KB for 256 x 768) is staged alongside, one
+// chunk ahead.  Per-row sums of squares and fp16-overflow flags come from the
+// same registers.  Measured (10M x 768, 256 queries, tools/filter_diag.py):
+// the X stream alone runs at 6.8 TB/s; re-reading the query tile from L2 for
+// every 256-row tile and the LDS staging cost ~1.3 ms of a ~6 ms pass, the
+// MFMAs (16 % of the fp16 peak) ~1 ms, the epilogue ~0.6 ms.
 #include "fx_internal.h"
 #include "fx_wave.h"
 
 namespace fx {
 
-constexpr int fBM = 128;                        // corpus rows per tile
+#ifndef FX_FILTER_WAVES
+#define FX_FILTER_WAVES 8   // waves per workgroup (two per SIMD)
+#endif
+#ifndef FX_FILTER_BPC
+#define FX_FILTER_BPC 1     // workgroups per CU (LDS and registers permitting)
+#endif
+#ifndef FX_FILTER_STAGES
+#define FX_FILTER_STAGES 2  // K chunks of X in flight per thread
+#endif
+#ifndef FX_FILTER_BM
+#define FX_FILTER_BM 256
+#endif
+#ifndef FX_FILTER_BK
+#define FX_FILTER_BK 32
+#endif
+constexpr int fBM = FX_FILTER_BM;               // corpus rows per tile
 constexpr int fBQ = 256;                        // queries per block
-constexpr int fBK = 64;                         // K chunk (elements)
-constexpr int fLds = fBK + 8;                   // padded LDS row (halves): 144 B
-constexpr int fThreads = 512;                   // 8 waves: 2 row groups x 4 query groups of 64
+constexpr int fBK = FX_FILTER_BK;               // K chunk (elements)
+constexpr int fLds = fBK + 8;                   // padded LDS row (halves): 16 B pad
+constexpr int fWaves = FX_FILTER_WAVES;
+constexpr int fThreads = 64 * fWaves;           // waves: fRG row groups x fQG query groups
+constexpr int fRG = fBM / 64;                   // 64-row groups (2 MFMA row tiles each)
+constexpr int fQG = fWaves / fRG;               // query groups
+constexpr int fQT = fBQ / fQG / 32;             // 32-query MFMA tiles per wave
+constexpr int fStages = FX_FILTER_STAGES;
 constexpr int fXC = fBK / 4;                    // 16-B f32 pieces per row per chunk
 constexpr int fQC = fBK / 8;                    // 16-B f16 pieces per query per chunk
-constexpr int fXP = fBM * fXC / fThreads;       // X pieces per thread per chunk: 4
-constexpr int fQP = fBQ * fQC / fThreads;       // Q pieces per thread per chunk: 4
+constexpr int fXP = fBM * fXC / fThreads;       // X pieces per thread per chunk
+constexpr int fQP = fBQ * fQC / fThreads;       // Q pieces per thread per chunk
 constexpr int fRowLanes = fXC;                  // lanes sharing one row's pieces
+static_assert(fQG >= 1 && fRG * fQG == fWaves && fQT >= 1, "wave grid");
+static_assert(fXP >= 1 && fQP >= 1 && fBK % 16 == 0, "staging");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -65,12 +91,14 @@ struct FilterShared {
   _Float16 xs[2][fBM * fLds];
   _Float16 qs[2][fBQ * fLds];
   float rinfo[fBM];  // per-row bound factor (see the epilogue)
+  f32x4 qtab[fBQ];   // per query: the bound's constants {c1, c0, A, B}
+  float2 qab[fBQ];   // per query: pass iff product >= a * row value + b
 };
 
-struct FilterPre {  // one chunk of X rows in flight (two of these: two chunks ahead)
+struct FilterPre {  // one K chunk of X rows in flight
   f32x4 x[fXP];
 };
-struct FilterPreQ {  // one chunk of the (L2-resident) query tile: one chunk ahead
+struct FilterPreQ {  // one K chunk of the (L2-resident) query tile
   i32x4 q[fQP];
 };
 
@@ -81,10 +109,24 @@ struct FilterAddr {
   int d, dq;
 };
 
+__device__ __forceinline__ void filter_load_q(FilterPreQ& p, const FilterAddr& ad, unsigned tid,
+                                              int c, int diag) {
+#pragma unroll
+  for (int i = 0; i < fQP; ++i) {
+    if (diag & 8) {
+      p.q[i] = i32x4(0);
+      continue;
+    }
+    const uint32_t off = (((i * fThreads + tid) / fQC) * (unsigned)ad.dq + (tid % fQC) * 8) * 2;
+    p.q[i] = __builtin_bit_cast(
+        i32x4, __builtin_amdgcn_raw_buffer_load_b128(ad.qr, off, c * fBK * 2, 0));
+  }
+}
+
 __device__ __forceinline__ void filter_load(FilterPre& p, const FilterAddr& ad, unsigned tid, int c) {
   const int k0 = c * fBK;
-  const unsigned c4 = tid % fXC;                  // this lane's 16-B piece of a row chunk
-  const bool in_row = k0 + (int)c4 * 4 < ad.d;   // past the row end: an offset beyond the buffer
+  const unsigned c4 = tid % fXC;                 // this lane's 16-B piece of a row chunk
+  const bool in_row = k0 + (int)c4 * 4 < ad.d;  // past the row end: an offset beyond the buffer
 #pragma unroll
   for (int i = 0; i < fXP; ++i) {
     const uint32_t off = (((i * fThreads + tid) / fXC) * (unsigned)ad.d + c4 * 4) * 4;
@@ -94,18 +136,9 @@ __device__ __forceinline__ void filter_load(FilterPre& p, const FilterAddr& ad, 
   }
 }
 
-__device__ __forceinline__ void filter_load_q(FilterPreQ& p, const FilterAddr& ad, unsigned tid, int c) {
-#pragma unroll
-  for (int i = 0; i < fQP; ++i) {
-    const uint32_t off = (((i * fThreads + tid) / fQC) * (unsigned)ad.dq + (tid % fQC) * 8) * 2;
-    p.q[i] = __builtin_bit_cast(
-        i32x4, __builtin_amdgcn_raw_buffer_load_b128(ad.qr, off, c * fBK * 2, 0));
-  }
-}
-
 __device__ __forceinline__ void filter_store(const FilterPre& p, const FilterPreQ& pq,
                                              FilterShared* sh, int buf, unsigned tid,
-                                             float (&sq)[fXP], float (&mx)[fXP]) {
+                                             float (&sq)[fXP], uint32_t& ovf) {
 #pragma unroll
   for (int i = 0; i < fXP; ++i) {
     const unsigned idx = i * fThreads + tid;
@@ -113,10 +146,10 @@ __device__ __forceinline__ void filter_store(const FilterPre& p, const FilterPre
     *reinterpret_cast<f16x4*>(&sh->xs[buf][(idx / fXC) * fLds + (idx % fXC) * 4]) =
         __builtin_convertvector(v, f16x4);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      sq[i] = fmaf(v[t], v[t], sq[i]);
-      mx[i] = fmaxf(mx[i], fabsf(v[t]));
-    }
+    for (int t = 0; t < 4; ++t) sq[i] = fmaf(v[t], v[t], sq[i]);
+    // a component that rounds to an fp16 infinity (|x| >= 65520)
+    const float m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+    ovf |= (uint32_t)(m >= 65520.f) << i;
   }
 #pragma unroll
   for (int i = 0; i < fQP; ++i) {
@@ -133,51 +166,97 @@ __device__ __forceinline__ unsigned opaque(unsigned v) {
   return v;
 }
 
-__device__ __forceinline__ void filter_compute(f32x16 (&acc)[2][2], const FilterShared* sh,
+__device__ __forceinline__ void filter_compute(f32x16 (&acc)[2][fQT], const FilterShared* sh,
                                                int buf, unsigned tid) {
   const unsigned lane = tid & 63, wid = tid >> 6;
-  const unsigned rg = wid & 1, qg = wid >> 1, h = lane >> 5, l32 = lane & 31;
+  const unsigned rg = wid % fRG, qg = wid / fRG, h = lane >> 5, l32 = lane & 31;
   const _Float16* xs = sh->xs[buf] + (rg * 64 + l32) * fLds + 8 * h;
-  const _Float16* qs = sh->qs[buf] + (qg * 64 + l32) * fLds + 8 * h;
+  const _Float16* qs = sh->qs[buf] + (qg * fQT * 32 + l32) * fLds + 8 * h;
 #pragma unroll
   for (int s = 0; s < fBK / 16; ++s) {
-    f16x8 av[2], bv[2];
+    f16x8 av[2], bv[fQT];
 #pragma unroll
     for (int t = 0; t < 2; ++t) av[t] = *reinterpret_cast<const f16x8*>(xs + t * 32 * fLds + 16 * s);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) bv[u] = *reinterpret_cast<const f16x8*>(qs + u * 32 * fLds + 16 * s);
+    for (int u = 0; u < fQT; ++u) bv[u] = *reinterpret_cast<const f16x8*>(qs + u * 32 * fLds + 16 * s);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < fQT; ++u)
         acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[t], bv[u], acc[t][u], 0, 0, 0);
   }
 }
 
 template <int METRIC>
-__global__ void __launch_bounds__(fThreads, 2) filter_kernel(FilterArgs a) {
+__global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_kernel(FilterArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   FilterShared* sh = reinterpret_cast<FilterShared*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int rg = wid & 1, qg = wid >> 1;  // 64-row group, 64-query group
+  const int rg = wid % fRG, qg = wid / fRG;  // 64-row group, fQT*32-query group
   const int h = lane >> 5, l32 = lane & 31;
   const int64_t q0 = (int64_t)blockIdx.y * fBQ;
   const int nch = (a.d + fBK - 1) / fBK;
   const int diag = a.diag;
+
+  // per-query constants (once per block).  The pass test lb <= T is linear in
+  // the product x for a fixed row, so it is precomputed as x >= a * rv + b
+  // with rv the row's value (cosine: max(|x|, 1e-12); IP: |x|; L2: |x|^2):
+  //   cos  lb = x c1 / rv + 0.5 - A - B / rv,  c1 = -0.5 / (scale |q|) < 0
+  //        -> x >= ((T - 0.5 + A) rv + B) / c1
+  //   IP   lb = -x / scale - A rv - B           -> x >= (-T - B - A rv) scale
+  //   L2   lb^2 = s2 - 2 x / scale - A s2 - B,  s2 = rv + |q|^2, against
+  //        T^2 (1 + 2^-20) -> x >= ((1 - A) s2 - B - T^2) scale / 2
+  // The roundings of this rearrangement are far inside the bound's slack.
+  // T = NaN (no threshold yet) or a forced query: everything passes
+  // (a = 0, b = -inf); padding queries: nothing (b = +inf).
+  for (int i = tid; i < fBQ; i += fThreads) {
+    const int64_t gq = q0 + i;
+    f32x4 c = f32x4(0.f);
+    float2 ab = {0.f, __builtin_inff()};
+    if (gq < a.nq) {
+      const f32x4 info = *reinterpret_cast<const f32x4*>(a.qinfo + gq * 4);
+      const float tf = key_float((uint32_t)(a.thr[gq] >> 32));
+      const float qinv = info[0], qa = info[1], qA = info[2], qB = info[3];
+      c[2] = qA;
+      c[3] = qB;
+      if constexpr (METRIC == 0) {
+        c[0] = -2.f * qinv;
+        c[1] = qa;
+        const float t2 = tf * tf * (1.f + 9.5367431640625e-07f);
+        const float h = 0.5f / qinv;
+        ab.x = (1.f - qA) * h;
+        ab.y = ((1.f - qA) * qa - qB - t2) * h;
+      } else if constexpr (METRIC == 1) {
+        c[0] = -qinv;
+        const float sc = 1.f / qinv;
+        ab.x = -qA * sc;
+        ab.y = (-tf - qB) * sc;
+      } else {
+        c[0] = -0.5f * qinv / qa;
+        ab.x = (tf - 0.5f + qA) / c[0];
+        ab.y = qB / c[0];
+      }
+      if (tf != tf || !(qA <= 3.4e38f)) ab = {0.f, -__builtin_inff()};
+    }
+    sh->qtab[i] = c;
+    sh->qab[i] = ab;
+  }
+  // (the first tile's barriers order these writes before the epilogue reads)
 
   for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x) {
     const int64_t tile = a.tile_start + ti * a.tile_stride;
     const int64_t r0 = tile * fBM;
     if (r0 >= a.n) continue;
 
-    f32x16 acc[2][2];
+    f32x16 acc[2][fQT];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) acc[t][u] = f32x16(0.f);
-    float sq[fXP], mx[fXP];
+      for (int u = 0; u < fQT; ++u) acc[t][u] = f32x16(0.f);
+    float sq[fXP];
 #pragma unroll
-    for (int i = 0; i < fXP; ++i) sq[i] = mx[i] = 0.f;
+    for (int i = 0; i < fXP; ++i) sq[i] = 0.f;
+    uint32_t ovf = 0u;
 
     const int64_t rows = a.n - r0 < fBM ? a.n - r0 : fBM;
     FilterAddr ad;
@@ -200,178 +279,165 @@ __global__ void __launch_bounds__(fThreads, 2) filter_kernel(FilterArgs a) {
       ad.dq = a.dq;
     }
 
-    // X: two register stages (chunks c + 2 and c + 3 in flight while chunk c is
-    // multiplied); Q (L2 hits): one stage.  Loads are issued unconditionally
-    // (chunks past the row end read as zeros through the descriptor bounds):
-    // a load under a branch makes the compiler wait for it where the branch
-    // joins, which would drain the pipeline every chunk.  Q is issued before
-    // X: waiting for Q(c + 2) next iteration must not wait for X(c + 3)
-    // (vmcnt retires loads in issue order).
-    FilterPre p0, p1;
+    // fStages register stages: chunks c + 2 .. c + fStages of X and Q are in
+    // flight while chunk c is multiplied (stage j % fStages holds chunk j).
+    // Loads are issued unconditionally (chunks past the row end read as zeros
+    // through the descriptor bounds): a load under a branch makes the compiler
+    // wait for it where the branch joins, draining the pipeline every chunk.
+    FilterPre pf[fStages];
     FilterPreQ pq;
-    filter_load(p0, ad, opaque(tid), 0);
-    filter_load_q(pq, ad, opaque(tid), 0);
-    filter_load(p1, ad, opaque(tid), 1);
-    filter_store(p0, pq, sh, 0, opaque(tid), sq, mx);
-    filter_load_q(pq, ad, opaque(tid), 1);
-    filter_load(p0, ad, opaque(tid), 2);
+#pragma unroll
+    for (int j = 0; j < fStages; ++j) {
+      if (j == 0) filter_load_q(pq, ad, opaque(tid), 0, diag);
+      filter_load(pf[j], ad, opaque(tid), j);
+    }
+    filter_store(pf[0], pq, sh, 0, opaque(tid), sq, ovf);
+    // Q one chunk ahead, issued before the X load of the same step: vmcnt
+    // retires loads in issue order, so waiting for Q(c + 1) at step c waits
+    // for X(c + 1) (needed there anyway) and nothing issued later.
+    filter_load_q(pq, ad, opaque(tid), 1, diag);
+    filter_load(pf[0], ad, opaque(tid), fStages);
     __syncthreads();
-    for (int c = 0; c < nch; c += 2) {
-      if (!(diag & 4)) filter_compute(acc, sh, 0, opaque(tid));
-      if (c + 1 < nch) filter_store(p1, pq, sh, 1, opaque(tid), sq, mx);
-      filter_load_q(pq, ad, opaque(tid), c + 2);
-      filter_load(p1, ad, opaque(tid), c + 3);
-      __syncthreads();
-      if (c + 1 >= nch) break;
-      if (!(diag & 4)) filter_compute(acc, sh, 1, opaque(tid));
-      if (c + 2 < nch) filter_store(p0, pq, sh, 0, opaque(tid), sq, mx);
-      filter_load_q(pq, ad, opaque(tid), c + 3);
-      filter_load(p0, ad, opaque(tid), c + 4);
-      __syncthreads();
+    for (int c0 = 0; c0 < nch; c0 += fStages) {
+#pragma unroll
+      for (int j = 0; j < fStages; ++j) {
+        const int c = c0 + j;
+        if (c >= nch) break;
+        if (!(diag & 4)) filter_compute(acc, sh, c & 1, opaque(tid));
+        if (c + 1 < nch && !(diag & 16))
+          filter_store(pf[(j + 1) % fStages], pq, sh, (c + 1) & 1, opaque(tid), sq, ovf);
+        filter_load_q(pq, ad, opaque(tid), c + 2, diag);
+        filter_load(pf[(j + 1) % fStages], ad, opaque(tid), c + 1 + fStages);
+        __syncthreads();
+      }
     }
 
-    // per-row bound factor from |x|^2 and max|x| (the fRowLanes lanes of a row
-    // hold partials): rinfo = the metric's row term, NaN = forced through
-    // (fp16 overflow, non-finite), -1 = skipped (past n or masked out)
+    // per-row value rv from |x|^2 (the fRowLanes lanes of a row hold partials):
+    // cosine max(|x|, 1e-12), IP |x|, L2 |x|^2; NaN = forced through (fp16
+    // overflow, non-finite); -1 = skipped (past n or masked out)
 #pragma unroll
     for (int i = 0; i < fXP; ++i) {
 #pragma unroll
-      for (int m = 1; m < fRowLanes; m <<= 1) {
-        sq[i] += __shfl_xor(sq[i], m);
-        mx[i] = fmaxf(mx[i], __shfl_xor(mx[i], m));
-      }
+      for (int m = 1; m < fRowLanes; m <<= 1) sq[i] += __shfl_xor(sq[i], m);
+    }
+#pragma unroll
+    for (int m = 1; m < fRowLanes; m <<= 1) ovf |= __shfl_xor(ovf, m);
+#pragma unroll
+    for (int i = 0; i < fXP; ++i) {
       if (tid % fRowLanes == 0) {
         const int lr = (i * fThreads + tid) / fXC;
         const int64_t row = r0 + lr;
         bool ok = row < a.n;
         if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
-        float rterm;
+        float rv;
         if constexpr (METRIC == 0) {
-          rterm = sq[i];
+          rv = sq[i];
         } else if constexpr (METRIC == 1) {
-          rterm = sqrtf(sq[i]);
+          rv = sqrtf(sq[i]);
         } else {
-          rterm = 1.f / fmaxf(sqrtf(sq[i]), 1e-12f);
+          rv = fmaxf(sqrtf(sq[i]), 1e-12f);
         }
-        if (!(mx[i] < 65504.f) || !(sq[i] <= 3.4e38f)) rterm = __builtin_nanf("");
-        sh->rinfo[lr] = ok ? rterm : -1.f;
+        if (!(sq[i] <= 3.4e38f) || ((ovf >> i) & 1u)) rv = __builtin_nanf("");
+        sh->rinfo[lr] = ok ? rv : -1.f;
       }
     }
     __syncthreads();
 
     // ---- epilogue: [lb, ub] per (row, query), threshold test, append
     if (diag & 2) {
-      if (acc[0][0][0] == 1.2345f && acc[1][1][5] == 2.f) a.count[0] = 7;
+      if (acc[0][0][0] == 1.2345f && acc[1][fQT - 1][5] == 2.f) a.count[0] = 7;
       continue;
     }
-    // Pass test per (row, query) in a few fused ops on a conservative form of
-    // lb <= threshold (extra passes only cost a rescored candidate); the lane's
-    // passes over its 32 rows are collected in a bit mask per query column.
-    // Forced rows (NaN row term) and forced queries (A = inf) pass by NaN/-inf.
+
+    // Pass test: one fma and a compare per (row, query) (see the table above;
+    // extra passes only cost a rescored candidate); the lane's passes over its
+    // 32 rows are collected in a bit mask per query column, one atomic per
+    // (lane, column) reserves their slots.  Forced rows always pass, skipped
+    // rows never.
     const int lr0 = rg * 64 + 4 * h;
     const float* ri = sh->rinfo + lr0;
-    uint32_t pm[2];
-    float qc1[2], qc0[2], qA[2], qB[2], qthr[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t gq = q0 + qg * 64 + u * 32 + l32;
-      const bool live = gq < a.nq;
-      const f32x4 info = live ? *reinterpret_cast<const f32x4*>(a.qinfo + gq * 4) : f32x4(0.f);
-      const float tf = live ? key_float((uint32_t)(a.thr[gq] >> 32)) : -__builtin_inff();
-      qA[u] = info[2];
-      qB[u] = info[3];
-      if constexpr (METRIC == 0) {
-        qc1[u] = -2.f * info[0];
-        qc0[u] = info[1];
-        qthr[u] = tf * tf * (1.f + 9.5367431640625e-07f);  // lb <= T  <=  lb^2 <= T^2 (1 + 2^-20)
-      } else if constexpr (METRIC == 1) {
-        qc1[u] = -info[0];
-        qthr[u] = tf;
-      } else {
-        qc1[u] = -0.5f * info[0] / info[1];
-        qthr[u] = tf;
-      }
-      pm[u] = 0u;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int off = t * 32 + (r & 3) + 8 * (r >> 2);  // compile-time row offset
-          const float rterm = ri[off];
-          const float x = acc[t][u][r];
-          float v;
-          if constexpr (METRIC == 0) {
-            const float s2 = rterm + qc0[u];
-            v = fmaf(x, qc1[u], s2) - fmaf(qA[u], s2, qB[u]);
-          } else if constexpr (METRIC == 1) {
-            v = fmaf(x, qc1[u], -fmaf(qA[u], rterm, qB[u]));
-          } else {
-            v = fmaf(x * rterm, qc1[u], 0.5f) - fmaf(qB[u], rterm, qA[u]);
-          }
-          // rterm < 0: skipped row (past n / masked out); NaN v passes
-          const bool pass = !(v > qthr[u]) && !(rterm < 0.f);
-          pm[u] |= (uint32_t)pass << (t * 16 + r);
-        }
-      }
-      if (!live || (diag & 1)) pm[u] = 0u;
-    }
-    // one atomic per (lane, query column) with passes: positions for all of them
-    uint32_t pos[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      pos[u] = 0u;
-      if (pm[u] != 0u) {
-        const int64_t gq = q0 + qg * 64 + u * 32 + l32;
-        pos[u] = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(pm[u]));
-      }
-    }
-    if (__ballot((pm[0] | pm[1]) != 0u) == 0ull) continue;
     const uint32_t grow0 = (uint32_t)(a.row_base + r0 + lr0);
+    float rvs[32];
+    uint32_t fmask = 0u, smask = 0u;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t gq = q0 + qg * 64 + u * 32 + l32;
-      const bool fq = !(qA[u] <= 3.4e38f);
+    for (int t = 0; t < 2; ++t) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int r = 0; r < 16; ++r) {
+        const float rv = ri[t * 32 + (r & 3) + 8 * (r >> 2)];  // compile-time row offset
+        rvs[t * 16 + r] = rv;
+        fmask |= (uint32_t)(rv != rv) << (t * 16 + r);
+        smask |= (uint32_t)(rv < 0.f) << (t * 16 + r);
+      }
+    }
+    uint32_t pm[fQT];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          if (!((pm[u] >> (t * 16 + r)) & 1u)) continue;
-          const int off = t * 32 + (r & 3) + 8 * (r >> 2);
-          const float rterm = ri[off];
-          const float x = acc[t][u][r];
-          float lb, ub;
-          if constexpr (METRIC == 0) {
-            const float s2 = rterm + qc0[u];
-            const float d2 = fmaf(x, qc1[u], s2);
-            const float e = fmaf(qA[u], s2, qB[u]);
-            lb = sqrtf(fmaxf(d2 - e, 0.f));
-            ub = sqrtf(d2 + e);
-          } else if constexpr (METRIC == 1) {
-            const float e = fmaf(qA[u], rterm, qB[u]);
-            lb = fmaf(x, qc1[u], -e);
-            ub = fmaf(x, qc1[u], e);
+    for (int u = 0; u < fQT; ++u) {
+      const float2 ab = sh->qab[qg * fQT * 32 + u * 32 + l32];
+      uint32_t m = 0u;
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        m |= (uint32_t)(acc[j >> 4][u][j & 15] >= fmaf(ab.x, rvs[j], ab.y)) << j;
+      pm[u] = (diag & 1) ? 0u : ((m | fmask) & ~smask);
+      if (q0 + qg * fQT * 32 + u * 32 + l32 >= a.nq) pm[u] = 0u;
+    }
+    uint32_t any = 0u;
+#pragma unroll
+    for (int u = 0; u < fQT; ++u) any |= pm[u];
+    if (__ballot(any != 0u) == 0ull) continue;
+    uint32_t pos[fQT];
+#pragma unroll
+    for (int u = 0; u < fQT; ++u) {
+      pos[u] = 0u;
+      const int64_t gq = q0 + qg * fQT * 32 + u * 32 + l32;
+      if (pm[u] != 0u) pos[u] = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(pm[u]));
+    }
+#pragma unroll
+    for (int u = 0; u < fQT; ++u) {
+      if (__ballot(pm[u] != 0u) == 0ull) continue;
+      const int qi = qg * fQT * 32 + u * 32 + l32;
+      const int64_t gq = q0 + qi;
+      const f32x4 qc = sh->qtab[qi];
+      const float qc1 = qc[0], qc0 = qc[1], qA = qc[2], qB = qc[3];
+      const bool fq = !(qA <= 3.4e38f);
+      uint32_t p = pos[u];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        if (!((pm[u] >> j) & 1u)) continue;
+        const float rv = rvs[j];
+        const float x = acc[j >> 4][u][j & 15];
+        float lb, ub;
+        if constexpr (METRIC == 0) {
+          const float s2 = rv + qc0;
+          const float d2 = fmaf(x, qc1, s2);
+          const float e = fmaf(qA, s2, qB);
+          lb = sqrtf(fmaxf(d2 - e, 0.f));
+          ub = sqrtf(d2 + e);
+        } else if constexpr (METRIC == 1) {
+          const float e = fmaf(qA, rv, qB);
+          lb = fmaf(x, qc1, -e);
+          ub = fmaf(x, qc1, e);
+        } else {
+          const float rterm = 1.f / rv;
+          const float dist = fmaf(x * rterm, qc1, 0.5f);
+          const float e = fmaf(qB, rterm, qA);
+          lb = dist - e;
+          ub = dist + e;
+        }
+        if (fq || rv != rv) {  // forced: below / above every key
+          lb = -__builtin_inff();
+          ub = __builtin_nanf("");
+        }
+        if (p < (uint32_t)a.cap) {
+          const uint32_t grow = grow0 + (uint32_t)(((j >> 4) * 32) + ((j & 15) & 3) + 8 * ((j & 15) >> 2));
+          const size_t slot = (size_t)gq * a.cap + p;
+          if (a.cand_ub != nullptr) {
+            a.cand[slot] = make_comp(lb, grow);
+            a.cand_ub[slot] = make_comp(ub, grow);
           } else {
-            const float dist = fmaf(x * rterm, qc1[u], 0.5f);
-            const float e = fmaf(qB[u], rterm, qA[u]);
-            lb = dist - e;
-            ub = dist + e;
-          }
-          if (fq || rterm != rterm) {  // forced: below / above every key
-            lb = -__builtin_inff();
-            ub = __builtin_nanf("");
-          }
-          const uint32_t p = pos[u]++;
-          if (p < (uint32_t)a.cap) {
-            const uint32_t grow = grow0 + (uint32_t)off;
-            const size_t slot = (size_t)gq * a.cap + p;
-            if (a.cand_ub != nullptr) {
-              a.cand[slot] = make_comp(lb, grow);
-              a.cand_ub[slot] = make_comp(ub, grow);
-            } else {
-              a.cand[slot] = make_comp(ub, grow);
-            }
+            a.cand[slot] = make_comp(ub, grow);
           }
         }
+        ++p;
       }
     }
   }
@@ -397,7 +463,7 @@ int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
   int rc = device_cus(&cus);
   if (rc) return rc;
   const int64_t qtiles = (a.nq + fBQ - 1) / fBQ;
-  int64_t bx = cus;
+  int64_t bx = (int64_t)cus * FX_FILTER_BPC;
   if (bx > a.num_tiles) bx = a.num_tiles;
   for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
     FilterArgs b = a;
