@@ -141,12 +141,16 @@ static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool align
   if (const char* env = getenv("FX_BATCH")) {
     if (atoi(env) == 0) return false;
   }
-  return nq >= kBatchMinQ && dtype == FX_DTYPE_F32 && d % 4 == 0 && aligned;
+  if (nq < kBatchMinQ || !aligned) return false;
+  // the rescoring repeats the scan's 16-B slot order: f32 rows need d % 4 == 0,
+  // f16 rows d % 8 == 0 and the fp16 filter in its LDS-DMA form
+  if (dtype == FX_DTYPE_F32) return d % 4 == 0;
+  return dtype == FX_DTYPE_F16 && d % 8 == 0 && use_filter();
 }
 
-static int plan_batched(int64_t n, int64_t d, int64_t nq, int64_t k, BatchLayout* b) {
+static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, BatchLayout* b) {
   b->filter = use_filter();
-  const int64_t tr = b->filter ? filter_tile_rows() : batch_tile_rows();
+  const int64_t tr = b->filter ? filter_tile_rows(dtype) : batch_tile_rows();
   b->cap = 64 * k > 16384 ? 64 * k : 16384;
   if (const char* env = getenv("FX_BATCH_CAP")) {  // test knob: small buffers
     const int64_t c = atoll(env);
@@ -248,7 +252,7 @@ static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, i
   int rc = plan_single(n, d, dtype, 1, k, metric, aligned, s);
   if (rc) return rc;
   const size_t single_total = s->total;
-  rc = plan_batched(n, d, nq, k, &s->batch);
+  rc = plan_batched(n, d, dtype, nq, k, &s->batch);
   if (rc) return rc;
   s->batched = true;
   s->single_off = s->batch.total;
@@ -296,7 +300,7 @@ static int single_search(const void* corpus, int dtype, int64_t n, int64_t d, in
 // threshold, and only candidates whose lower bound reaches it are rescored
 // exactly (the rest are dropped unread).  fx_knn_reduce then selects the top k
 // of the exact keys and recomputes overflowing queries.
-static int filter_phases(const BatchLayout& b, const float* X, int64_t n, int64_t d,
+static int filter_phases(const BatchLayout& b, const void* X, int dtype, int64_t n, int64_t d,
                          int64_t row_base, const float* Q, int64_t nq, int metric, int64_t k,
                          const uint32_t* mask, char* w, hipStream_t st) {
   float* qnorm = reinterpret_cast<float*>(w + b.off_qnorm);
@@ -321,6 +325,7 @@ static int filter_phases(const BatchLayout& b, const float* X, int64_t n, int64_
     if (e != hipSuccess) break;
     FilterArgs a = {};
     a.X = X;
+    a.dtype = dtype;
     a.n = n;
     a.d = (int)d;
     a.row_base = row_base;
@@ -349,8 +354,8 @@ static int filter_phases(const BatchLayout& b, const float* X, int64_t n, int64_
     set_error("batched memset: %s", hipGetErrorString(e));
     return FX_EHIP;
   }
-  return launch_rescore(X, n, (int)d, row_base, Q, qnorm, nq, count, cand, (int)b.cap, metric,
-                        thr, st);
+  return launch_rescore(X, dtype, n, (int)d, row_base, Q, qnorm, nq, count, cand, (int)b.cap,
+                        metric, thr, st);
 }
 
 static int batched_phases(const BatchLayout& b, const float* X, int64_t n, int64_t d,
@@ -391,8 +396,8 @@ static int batched_phases(const BatchLayout& b, const float* X, int64_t n, int64
     rc = launch_batch(a, metric, st);
     if (rc) return rc;
     if (l2) {  // approximate keys -> exact distances before any select
-      rc = launch_rescore(X, n, (int)d, row_base, Q, nullptr, nq, count, cand, (int)b.cap,
-                          FX_METRIC_L2, nullptr, st);
+      rc = launch_rescore(X, FX_DTYPE_F32, n, (int)d, row_base, Q, nullptr, nq, count, cand,
+                          (int)b.cap, FX_METRIC_L2, nullptr, st);
       if (rc) return rc;
     }
     if (ph + 1 < b.nphases) {
@@ -497,8 +502,8 @@ int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (s.batched) {
     if (s.batch.filter) {
-      return filter_phases(s.batch, reinterpret_cast<const float*>(corpus), n, d, row_base,
-                           queries, nq, metric, k, mask, reinterpret_cast<char*>(ws), st);
+      return filter_phases(s.batch, corpus, dtype, n, d, row_base, queries, nq, metric, k, mask,
+                           reinterpret_cast<char*>(ws), st);
     }
     return batched_phases(s.batch, reinterpret_cast<const float*>(corpus), n, d, row_base,
                           queries, nq, metric, k, mask, reinterpret_cast<char*>(ws), st);

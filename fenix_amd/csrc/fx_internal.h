@@ -82,14 +82,15 @@ int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stre
 // summation order: bit-identical).  thr (optional): candidates whose key is
 // above the query's thr key are dropped (kEmpty) without being read.
 // qnorm: cosine only, max(|q|, 1e-12) as the scan computes it.
-int launch_rescore(const float* X, int64_t n, int d, int64_t row_base, const float* Q,
-                   const float* qnorm, int64_t nq, const uint32_t* count, uint64_t* cand,
-                   int cap, int metric, const uint64_t* thr, hipStream_t stream);
+int launch_rescore(const void* X, int dtype, int64_t n, int d, int64_t row_base,
+                   const float* Q, const float* qnorm, int64_t nq, const uint32_t* count,
+                   uint64_t* cand, int cap, int metric, const uint64_t* thr, hipStream_t stream);
 
 // Batched filter on the fp16 matrix cores (knn_filter.hip): appends every
 // (row, query) whose rigorous lower bound reaches the query's threshold.
 struct FilterArgs {
-  const float* X;         // [n][d] f32 corpus shard
+  const void* X;          // [n][d] corpus shard (f32; f16 with the ring kernel)
+  int dtype;              // FX_DTYPE_F32 / FX_DTYPE_F16
   int64_t n;
   int d;
   int64_t row_base;
@@ -108,9 +109,12 @@ struct FilterArgs {
                           // 4 no MFMA, 8 no query loads, 16 no LDS stores
 };
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream);
+// the LDS-DMA ring variant (knn_filter.hip ring_kernel): always for f16 rows,
+// for f32 rows with FX_FILTER_RING=1 (the register-staged kernel otherwise)
+bool filter_ring();
 int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
                  uint16_t* Qh, float* qinfo, hipStream_t stream);
-int filter_tile_rows();
+int filter_tile_rows(int dtype);
 int filter_query_pad();
 int filter_dq(int d);
 int batch_tile_rows();

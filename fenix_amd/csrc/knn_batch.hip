@@ -296,14 +296,18 @@ int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stre
 // place (row unchanged).  With thr, a candidate whose (lower-bound) key is
 // above the query's threshold key is dropped unread.  Every lane of a wave
 // runs the same number of iterations (sum16 is a cross-lane reduction).
-template <int METRIC>
-__global__ void __launch_bounds__(256) rescore_kernel(const float* __restrict__ X, int64_t n, int d,
+template <typename T, int METRIC>
+__global__ void __launch_bounds__(256) rescore_kernel(const T* __restrict__ X, int64_t n, int d,
                                                       int64_t row_base,
                                                       const float* __restrict__ Q,
                                                       const float* __restrict__ qnorm,
                                                       const uint32_t* __restrict__ count,
                                                       uint64_t* __restrict__ cand, int cap,
                                                       const uint64_t* __restrict__ thr) {
+  // the scan's 16-B slots: 4 floats (f32) or 8 halves (f16), lane jl takes
+  // slots jl, jl + 16, ... (knn_scan.hip plan_scan: W = 16 / sizeof(T))
+  constexpr int W = 16 / sizeof(T);
+  typedef T vT __attribute__((ext_vector_type(W)));
   const int64_t q = blockIdx.y;
   const int lane = threadIdx.x & 63;
   const int grp = lane >> 4, jl = lane & 15;
@@ -321,20 +325,21 @@ __global__ void __launch_bounds__(256) rescore_kernel(const float* __restrict__ 
     const bool live = keep && row >= 0 && row < n;
     float acc = 0.f, acc2 = 0.f;
     if (live) {
-      const float* xr = X + row * (int64_t)d;
-      for (int k = jl * 4; k < d; k += 64) {
-        const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + k);
-        const f32x4 yv = *reinterpret_cast<const f32x4*>(qv + k);
+      const T* xr = X + row * (int64_t)d;
+      for (int k = jl * W; k < d; k += 16 * W) {
+        const vT xv = *reinterpret_cast<const vT*>(xr + k);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < W; ++t) {
+          const float x = (float)xv[t];
+          const float y = qv[k + t];
           if constexpr (METRIC == 0) {
-            const float df = xv[t] - yv[t];
+            const float df = x - y;
             acc = fmaf(df, df, acc);
           } else if constexpr (METRIC == 1) {
-            acc = fmaf(xv[t], yv[t], acc);
+            acc = fmaf(x, y, acc);
           } else {
-            acc = fmaf(xv[t], yv[t], acc);
-            acc2 = fmaf(xv[t], xv[t], acc2);
+            acc = fmaf(x, y, acc);
+            acc2 = fmaf(x, x, acc2);
           }
         }
       }
@@ -356,7 +361,23 @@ __global__ void __launch_bounds__(256) rescore_kernel(const float* __restrict__ 
   }
 }
 
-int launch_rescore(const float* X, int64_t n, int d, int64_t row_base, const float* Q,
+template <typename T>
+static void launch_rescore_t(const T* X, int64_t n, int d, int64_t row_base, const float* Q,
+                             const float* qnm, const uint32_t* count, uint64_t* cand, int cap,
+                             int metric, const uint64_t* t, dim3 grid, hipStream_t stream) {
+  if (metric == FX_METRIC_COS) {
+    hipLaunchKernelGGL((rescore_kernel<T, 2>), grid, dim3(256), 0, stream, X, n, d, row_base, Q,
+                       qnm, count, cand, cap, t);
+  } else if (metric == FX_METRIC_IP) {
+    hipLaunchKernelGGL((rescore_kernel<T, 1>), grid, dim3(256), 0, stream, X, n, d, row_base, Q,
+                       qnm, count, cand, cap, t);
+  } else {
+    hipLaunchKernelGGL((rescore_kernel<T, 0>), grid, dim3(256), 0, stream, X, n, d, row_base, Q,
+                       qnm, count, cand, cap, t);
+  }
+}
+
+int launch_rescore(const void* X, int dtype, int64_t n, int d, int64_t row_base, const float* Q,
                    const float* qnorm, int64_t nq, const uint32_t* count, uint64_t* cand,
                    int cap, int metric, const uint64_t* thr, hipStream_t stream) {
   int cus = 0;
@@ -369,15 +390,14 @@ int launch_rescore(const float* X, int64_t n, int d, int64_t row_base, const flo
     const dim3 grid((unsigned)bx, (unsigned)qn);
     const uint64_t* t = thr != nullptr ? thr + q0 : nullptr;
     const float* qnm = qnorm != nullptr ? qnorm + q0 : nullptr;
-    if (metric == FX_METRIC_COS) {
-      hipLaunchKernelGGL(rescore_kernel<2>, grid, dim3(256), 0, stream, X, n, d, row_base,
-                         Q + q0 * d, qnm, count + q0 * kCountStride, cand + q0 * (int64_t)cap, cap, t);
-    } else if (metric == FX_METRIC_IP) {
-      hipLaunchKernelGGL(rescore_kernel<1>, grid, dim3(256), 0, stream, X, n, d, row_base,
-                         Q + q0 * d, qnm, count + q0 * kCountStride, cand + q0 * (int64_t)cap, cap, t);
+    const uint32_t* cn = count + q0 * kCountStride;
+    uint64_t* cd = cand + q0 * (int64_t)cap;
+    if (dtype == FX_DTYPE_F16) {
+      launch_rescore_t(reinterpret_cast<const _Float16*>(X), n, d, row_base, Q + q0 * d, qnm, cn,
+                       cd, cap, metric, t, grid, stream);
     } else {
-      hipLaunchKernelGGL(rescore_kernel<0>, grid, dim3(256), 0, stream, X, n, d, row_base,
-                         Q + q0 * d, qnm, count + q0 * kCountStride, cand + q0 * (int64_t)cap, cap, t);
+      launch_rescore_t(reinterpret_cast<const float*>(X), n, d, row_base, Q + q0 * d, qnm, cn, cd,
+                       cap, metric, t, grid, stream);
     }
     rc = check_launch("rescore_kernel");
     if (rc) return rc;

@@ -187,29 +187,23 @@ __device__ __forceinline__ void filter_compute(f32x16 (&acc)[2][fQT], const Filt
   }
 }
 
+// Per-query constants of the pass test (once per block).  The test lb <= T
+// is linear in the product x for a fixed row, so it is precomputed as
+// x >= a * rv + b with rv the row's value (cosine: max(|x|, 1e-12); IP: |x|;
+// L2: |x|^2):
+//   cos  lb = x c1 / rv + 0.5 - A - B / rv,  c1 = -0.5 / (scale |q|) < 0
+//        -> x >= ((T - 0.5 + A) rv + B) / c1
+//   IP   lb = -x / scale - A rv - B           -> x >= (-T - B - A rv) scale
+//   L2   lb^2 = s2 - 2 x / scale - A s2 - B,  s2 = rv + |q|^2, against
+//        T^2 (1 + 2^-20) -> x >= ((1 - A) s2 - B - T^2) scale / 2
+// The roundings of this rearrangement are far inside the bound's slack.
+// T = NaN (no threshold yet) or a forced query: everything passes
+// (a = 0, b = -inf); padding queries: nothing (b = +inf).  qtab keeps
+// {c1, c0, A, B} for the exact bounds of appended pairs.
 template <int METRIC>
-__global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_kernel(FilterArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  FilterShared* sh = reinterpret_cast<FilterShared*>(smem);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int rg = wid % fRG, qg = wid / fRG;  // 64-row group, fQT*32-query group
-  const int h = lane >> 5, l32 = lane & 31;
-  const int64_t q0 = (int64_t)blockIdx.y * fBQ;
-  const int nch = (a.d + fBK - 1) / fBK;
-  const int diag = a.diag;
-
-  // per-query constants (once per block).  The pass test lb <= T is linear in
-  // the product x for a fixed row, so it is precomputed as x >= a * rv + b
-  // with rv the row's value (cosine: max(|x|, 1e-12); IP: |x|; L2: |x|^2):
-  //   cos  lb = x c1 / rv + 0.5 - A - B / rv,  c1 = -0.5 / (scale |q|) < 0
-  //        -> x >= ((T - 0.5 + A) rv + B) / c1
-  //   IP   lb = -x / scale - A rv - B           -> x >= (-T - B - A rv) scale
-  //   L2   lb^2 = s2 - 2 x / scale - A s2 - B,  s2 = rv + |q|^2, against
-  //        T^2 (1 + 2^-20) -> x >= ((1 - A) s2 - B - T^2) scale / 2
-  // The roundings of this rearrangement are far inside the bound's slack.
-  // T = NaN (no threshold yet) or a forced query: everything passes
-  // (a = 0, b = -inf); padding queries: nothing (b = +inf).
-  for (int i = tid; i < fBQ; i += fThreads) {
+__device__ __forceinline__ void filter_query_table(const FilterArgs& a, int64_t q0, f32x4* qtab,
+                                                   float2* qab, int tid, int nthreads) {
+  for (int i = tid; i < fBQ; i += nthreads) {
     const int64_t gq = q0 + i;
     f32x4 c = f32x4(0.f);
     float2 ab = {0.f, __builtin_inff()};
@@ -238,9 +232,119 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
       }
       if (tf != tf || !(qA <= 3.4e38f)) ab = {0.f, -__builtin_inff()};
     }
-    sh->qtab[i] = c;
-    sh->qab[i] = ab;
+    qtab[i] = c;
+    qab[i] = ab;
   }
+}
+
+// Epilogue of one tile: pass test per (row, query) — one fma and a compare
+// (see filter_query_table; extra passes only cost a rescored candidate); the
+// lane's passes over its 32 rows are collected in a bit mask per query
+// column, one atomic per (lane, column) reserves their slots.  Forced rows
+// (rinfo NaN) always pass, skipped rows (rinfo < 0) never.
+template <int METRIC, int QT>
+__device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], const float* rinfo,
+                                                const f32x4* qtab, const float2* qab,
+                                                const FilterArgs& a, int64_t q0, int64_t r0,
+                                                int rg, int qg, int h, int l32, int diag) {
+    const int lr0 = rg * 64 + 4 * h;
+    const float* ri = rinfo + lr0;
+    const uint32_t grow0 = (uint32_t)(a.row_base + r0 + lr0);
+    // row j of the lane (acc register j & 15 of row tile j >> 4) sits at a
+    // compile-time offset from ri: row values are re-read from LDS where used
+    auto roff = [](int j) { return (j >> 4) * 32 + (j & 3) + 8 * ((j & 15) >> 2); };
+    uint32_t fmask = 0u, smask = 0u;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const float rv = ri[roff(j)];
+      fmask |= (uint32_t)(rv != rv) << j;
+      smask |= (uint32_t)(rv < 0.f) << j;
+    }
+    uint32_t pm[QT];
+#pragma unroll
+    for (int u = 0; u < QT; ++u) {
+      const float2 ab = qab[qg * QT * 32 + u * 32 + l32];
+      uint32_t m = 0u;
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        m |= (uint32_t)(acc[j >> 4][u][j & 15] >= fmaf(ab.x, ri[roff(j)], ab.y)) << j;
+      pm[u] = (diag & 1) ? 0u : ((m | fmask) & ~smask);
+      if (q0 + qg * QT * 32 + u * 32 + l32 >= a.nq) pm[u] = 0u;
+    }
+    uint32_t any = 0u;
+#pragma unroll
+    for (int u = 0; u < QT; ++u) any |= pm[u];
+    if (__ballot(any != 0u) == 0ull) return;
+    uint32_t pos[QT];
+#pragma unroll
+    for (int u = 0; u < QT; ++u) {
+      pos[u] = 0u;
+      const int64_t gq = q0 + qg * QT * 32 + u * 32 + l32;
+      if (pm[u] != 0u) pos[u] = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(pm[u]));
+    }
+#pragma unroll
+    for (int u = 0; u < QT; ++u) {
+      if (__ballot(pm[u] != 0u) == 0ull) continue;
+      const int qi = qg * QT * 32 + u * 32 + l32;
+      const int64_t gq = q0 + qi;
+      const f32x4 qc = qtab[qi];
+      const float qc1 = qc[0], qc0 = qc[1], qA = qc[2], qB = qc[3];
+      const bool fq = !(qA <= 3.4e38f);
+      uint32_t p = pos[u];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        if (!((pm[u] >> j) & 1u)) continue;
+        const float rv = ri[roff(j)];
+        const float x = acc[j >> 4][u][j & 15];
+        float lb, ub;
+        if constexpr (METRIC == 0) {
+          const float s2 = rv + qc0;
+          const float d2 = fmaf(x, qc1, s2);
+          const float e = fmaf(qA, s2, qB);
+          lb = sqrtf(fmaxf(d2 - e, 0.f));
+          ub = sqrtf(d2 + e);
+        } else if constexpr (METRIC == 1) {
+          const float e = fmaf(qA, rv, qB);
+          lb = fmaf(x, qc1, -e);
+          ub = fmaf(x, qc1, e);
+        } else {
+          const float rterm = 1.f / rv;
+          const float dist = fmaf(x * rterm, qc1, 0.5f);
+          const float e = fmaf(qB, rterm, qA);
+          lb = dist - e;
+          ub = dist + e;
+        }
+        if (fq || rv != rv) {  // forced: below / above every key
+          lb = -__builtin_inff();
+          ub = __builtin_nanf("");
+        }
+        if (p < (uint32_t)a.cap) {
+          const uint32_t grow = grow0 + (uint32_t)roff(j);
+          const size_t slot = (size_t)gq * a.cap + p;
+          if (a.cand_ub != nullptr) {
+            a.cand[slot] = make_comp(lb, grow);
+            a.cand_ub[slot] = make_comp(ub, grow);
+          } else {
+            a.cand[slot] = make_comp(ub, grow);
+          }
+        }
+        ++p;
+      }
+    }
+}
+
+template <int METRIC>
+__global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_kernel(FilterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  FilterShared* sh = reinterpret_cast<FilterShared*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int rg = wid % fRG, qg = wid / fRG;  // 64-row group, fQT*32-query group
+  const int h = lane >> 5, l32 = lane & 31;
+  const int64_t q0 = (int64_t)blockIdx.y * fBQ;
+  const int nch = (a.d + fBK - 1) / fBK;
+  const int diag = a.diag;
+
+  filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
   // (the first tile's barriers order these writes before the epilogue reads)
 
   for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x) {
@@ -261,7 +365,7 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     const int64_t rows = a.n - r0 < fBM ? a.n - r0 : fBM;
     FilterAddr ad;
     {
-      const float* xb = a.X + r0 * (int64_t)a.d;
+      const float* xb = reinterpret_cast<const float*>(a.X) + r0 * (int64_t)a.d;
       const uint64_t xp = reinterpret_cast<uint64_t>(xb);
       const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xp);
       const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xp >> 32));
@@ -349,102 +453,326 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
       continue;
     }
 
-    // Pass test: one fma and a compare per (row, query) (see the table above;
-    // extra passes only cost a rescored candidate); the lane's passes over its
-    // 32 rows are collected in a bit mask per query column, one atomic per
-    // (lane, column) reserves their slots.  Forced rows always pass, skipped
-    // rows never.
-    const int lr0 = rg * 64 + 4 * h;
-    const float* ri = sh->rinfo + lr0;
-    const uint32_t grow0 = (uint32_t)(a.row_base + r0 + lr0);
-    float rvs[32];
-    uint32_t fmask = 0u, smask = 0u;
+    filter_epilogue<METRIC, fQT>(acc, sh->rinfo, sh->qtab, sh->qab, a, q0, r0, rg, qg, h, l32,
+                                 diag);
+  }
+}
+
+// ------------------------------------------------------------- LDS-DMA ring
+//
+// The same filter with every operand staged by LDS-DMA (buffer_load ... lds):
+// no prefetch registers, a 3-deep ring of K-chunk stages (X rows and the query
+// tile, 48 KB per stage for f32 rows), one raw s_barrier per chunk behind a
+// COUNTED vmcnt so two stages stay in flight across it (a __syncthreads()
+// would drain them: cdna_hip_programming.md §5 "Pipelining across barriers").
+// The stage sequence runs on across tiles, so the next tile's first chunks
+// stream in while a tile's epilogue runs.  Rows are converted to fp16 at
+// fragment-read time (f32 corpora) or read as they are (f16 corpora: exact).
+// LDS images are XOR-swizzled by 16-B piece (the DMA writes lane L at
+// base + 16 L; the swizzle is applied to the global address) so fragment
+// reads are bank-conflict free.
+namespace ring {
+#ifndef FX_RING_WAVES
+#define FX_RING_WAVES 16  // 4 per SIMD: 64 accumulator registers per wave
+#endif
+constexpr int kBM = 256, kBQ = 256, kBK = 32, kStages = 3, kWaves = FX_RING_WAVES;
+constexpr int kThreads = kWaves * 64;
+constexpr int kRG = 4;                  // 64-row groups
+constexpr int kQG = kWaves / kRG;       // query groups
+constexpr int kQT = kBQ / kQG / 32;     // 32-query tiles per wave
+template <typename XT>
+struct Lay {
+  static constexpr int xrow = kBK * (int)sizeof(XT);  // bytes per row per stage
+  static constexpr int xbytes = kBM * xrow;
+  static constexpr int qbytes = kBQ * kBK * 2;
+  static constexpr int stage = xbytes + qbytes;
+  static constexpr int xdma = xbytes / 1024 / kWaves;  // 1 KB DMA instructions per wave
+  static constexpr int qdma = qbytes / 1024 / kWaves;
+  static constexpr int ndma = xdma + qdma;
+  static constexpr int rinfo = kStages * stage;
+  static constexpr int qtab = rinfo + kBM * 4;
+  static constexpr int qab = qtab + kBQ * 16;
+  static constexpr int total = qab + kBQ * 8;
+};
+
+typedef __attribute__((address_space(3))) void* lds_ptr;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64_t bytes) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                           nb, 0x00020000);
+}
+
+// Issue the DMA of K chunk c of the tile at row r0 (and of the query tile)
+// into stage buffer sb.  Rows past n read as zeros (descriptor size), pieces
+// past d through an offset beyond it; a tile index past the end gets an empty
+// descriptor, so every wave always issues exactly Lay::ndma instructions.
+template <typename XT>
+__device__ __forceinline__ void ring_issue(unsigned char* smem, const FilterArgs& a, int64_t r0,
+                                           bool valid, int c, int sb, int wid, int lane,
+                                           __amdgpu_buffer_rsrc_t qr) {
+  using L = Lay<XT>;
+  const int64_t rows = valid ? (a.n - r0 < kBM ? a.n - r0 : kBM) : 0;
+  const __amdgpu_buffer_rsrc_t xr =
+      make_rsrc(reinterpret_cast<const XT*>(a.X) + (valid ? r0 : 0) * (int64_t)a.d,
+                rows * a.d * (int64_t)sizeof(XT));
+  const int k0 = c * kBK;
+  unsigned char* st = smem + sb * L::stage;
+#pragma unroll
+  for (int i = 0; i < L::xdma; ++i) {
+    const int j = wid * L::xdma + i;  // 1-KB block of the stage's X image
+    uint32_t voff;
+    if constexpr (sizeof(XT) == 4) {  // 8 rows x 8 pieces of 16 B per block
+      const int row = 8 * j + (lane >> 3);
+      const int p = (lane & 7) ^ ((row >> 1) & 7);
+      voff = k0 + p * 4 < a.d ? (uint32_t)((row * a.d + p * 4) * 4) : 0x7fff0000u;
+    } else {  // 16 rows x 4 pieces
+      const int row = 16 * j + (lane >> 2);
+      const int p = (lane & 3) ^ ((row >> 2) & 3);
+      voff = k0 + p * 8 < a.d ? (uint32_t)((row * a.d + p * 8) * 2) : 0x7fff0000u;
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr)(st + j * 1024), 16, voff,
+                                             k0 * (int)sizeof(XT), 0, 2 /* nt */);
+  }
+#pragma unroll
+  for (int i = 0; i < L::qdma; ++i) {
+    const int j = wid * L::qdma + i;  // 16 queries x 4 pieces per block
+    const int q = 16 * j + (lane >> 2);
+    const int p = (lane & 3) ^ ((q >> 2) & 3);
+    const uint32_t voff = (uint32_t)((q * a.dq + p * 8) * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (lds_ptr)(st + L::xbytes + j * 1024), 16, voff,
+                                             k0 * 2, 0, 0);
+  }
+}
+
+// MFMAs of one stage: 2 k-steps x (2 row tiles x 4 query tiles).  Waves of
+// query group 0 also accumulate the rows' sums of squares and fp16-overflow
+// flags from the values they read.
+// kv = d - (first k of the chunk): elements at k >= d are zeroed (the DMA of a
+// piece past the row end is dropped, leaving stale LDS there; the query tile
+// is zero-padded, but the row sums must not see it).
+template <typename XT>
+__device__ __forceinline__ void ring_compute(f32x16 (&acc)[2][kQT], const unsigned char* st,
+                                             int rg, int qg, int l32, int h, int kv,
+                                             float (&sq)[2], uint32_t& ovf) {
+  using L = Lay<XT>;
+#pragma unroll
+  for (int s = 0; s < kBK / 16; ++s) {
+    f16x8 av[2], bv[kQT];
+    const int kf = 16 * s + 8 * h;  // first k of this lane's fragment, relative to the chunk
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
+      const int R = rg * 64 + t * 32 + l32;
+      if constexpr (sizeof(XT) == 4) {
+        const int p0 = 4 * s + 2 * h, sw = (R >> 1) & 7;
+        f32x4 a0 = *reinterpret_cast<const f32x4*>(st + R * L::xrow + ((p0 ^ sw) * 16));
+        f32x4 a1 = *reinterpret_cast<const f32x4*>(st + R * L::xrow + (((p0 + 1) ^ sw) * 16));
+        if (kf >= kv) a0 = f32x4(0.f);
+        if (kf + 4 >= kv) a1 = f32x4(0.f);
+        const f16x4 c0 = __builtin_convertvector(a0, f16x4);
+        const f16x4 c1 = __builtin_convertvector(a1, f16x4);
+        av[t] = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
+        if (qg == 0) {
+          float m = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float rv = ri[t * 32 + (r & 3) + 8 * (r >> 2)];  // compile-time row offset
-        rvs[t * 16 + r] = rv;
-        fmask |= (uint32_t)(rv != rv) << (t * 16 + r);
-        smask |= (uint32_t)(rv < 0.f) << (t * 16 + r);
-      }
-    }
-    uint32_t pm[fQT];
-#pragma unroll
-    for (int u = 0; u < fQT; ++u) {
-      const float2 ab = sh->qab[qg * fQT * 32 + u * 32 + l32];
-      uint32_t m = 0u;
-#pragma unroll
-      for (int j = 0; j < 32; ++j)
-        m |= (uint32_t)(acc[j >> 4][u][j & 15] >= fmaf(ab.x, rvs[j], ab.y)) << j;
-      pm[u] = (diag & 1) ? 0u : ((m | fmask) & ~smask);
-      if (q0 + qg * fQT * 32 + u * 32 + l32 >= a.nq) pm[u] = 0u;
-    }
-    uint32_t any = 0u;
-#pragma unroll
-    for (int u = 0; u < fQT; ++u) any |= pm[u];
-    if (__ballot(any != 0u) == 0ull) continue;
-    uint32_t pos[fQT];
-#pragma unroll
-    for (int u = 0; u < fQT; ++u) {
-      pos[u] = 0u;
-      const int64_t gq = q0 + qg * fQT * 32 + u * 32 + l32;
-      if (pm[u] != 0u) pos[u] = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(pm[u]));
-    }
-#pragma unroll
-    for (int u = 0; u < fQT; ++u) {
-      if (__ballot(pm[u] != 0u) == 0ull) continue;
-      const int qi = qg * fQT * 32 + u * 32 + l32;
-      const int64_t gq = q0 + qi;
-      const f32x4 qc = sh->qtab[qi];
-      const float qc1 = qc[0], qc0 = qc[1], qA = qc[2], qB = qc[3];
-      const bool fq = !(qA <= 3.4e38f);
-      uint32_t p = pos[u];
-#pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        if (!((pm[u] >> j) & 1u)) continue;
-        const float rv = rvs[j];
-        const float x = acc[j >> 4][u][j & 15];
-        float lb, ub;
-        if constexpr (METRIC == 0) {
-          const float s2 = rv + qc0;
-          const float d2 = fmaf(x, qc1, s2);
-          const float e = fmaf(qA, s2, qB);
-          lb = sqrtf(fmaxf(d2 - e, 0.f));
-          ub = sqrtf(d2 + e);
-        } else if constexpr (METRIC == 1) {
-          const float e = fmaf(qA, rv, qB);
-          lb = fmaf(x, qc1, -e);
-          ub = fmaf(x, qc1, e);
-        } else {
-          const float rterm = 1.f / rv;
-          const float dist = fmaf(x * rterm, qc1, 0.5f);
-          const float e = fmaf(qB, rterm, qA);
-          lb = dist - e;
-          ub = dist + e;
-        }
-        if (fq || rv != rv) {  // forced: below / above every key
-          lb = -__builtin_inff();
-          ub = __builtin_nanf("");
-        }
-        if (p < (uint32_t)a.cap) {
-          const uint32_t grow = grow0 + (uint32_t)(((j >> 4) * 32) + ((j & 15) & 3) + 8 * ((j & 15) >> 2));
-          const size_t slot = (size_t)gq * a.cap + p;
-          if (a.cand_ub != nullptr) {
-            a.cand[slot] = make_comp(lb, grow);
-            a.cand_ub[slot] = make_comp(ub, grow);
-          } else {
-            a.cand[slot] = make_comp(ub, grow);
+          for (int e = 0; e < 4; ++e) {
+            sq[t] = fmaf(a0[e], a0[e], sq[t]);
+            sq[t] = fmaf(a1[e], a1[e], sq[t]);
+            m = fmaxf(m, fmaxf(fabsf(a0[e]), fabsf(a1[e])));
           }
+          ovf |= (uint32_t)(m >= 65520.f) << t;
         }
-        ++p;
+      } else {
+        const int p = 2 * s + h;
+        av[t] = *reinterpret_cast<const f16x8*>(st + R * L::xrow + ((p ^ ((R >> 2) & 3)) * 16));
+        if (kf >= kv) av[t] = f16x8(0);
+        if (qg == 0) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sq[t] = fmaf((float)av[t][e], (float)av[t][e], sq[t]);
+        }
       }
+    }
+#pragma unroll
+    for (int u = 0; u < kQT; ++u) {
+      const int Q = qg * kQT * 32 + u * 32 + l32;
+      const int p = 2 * s + h;
+      bv[u] = *reinterpret_cast<const f16x8*>(st + L::xbytes + Q * 64 + ((p ^ ((Q >> 2) & 3)) * 16));
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < kQT; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[t], bv[u], acc[t][u], 0, 0, 0);
+  }
+}
+
+// Wait until this wave's DMAs of the stage to be read have landed (the last
+// N issued stay in flight), then the workgroup barrier: every wave's DMAs of
+// that stage are in, and every wave is done reading the stage being refilled.
+template <int N>
+__device__ __forceinline__ void ring_sync() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+}  // namespace ring
+
+template <typename XT, int METRIC>
+__global__ void __launch_bounds__(ring::kThreads, ring::kWaves / 4) ring_kernel(FilterArgs a) {
+  using namespace ring;
+  using L = Lay<XT>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* rinfo = reinterpret_cast<float*>(smem + L::rinfo);
+  f32x4* qtab = reinterpret_cast<f32x4*>(smem + L::qtab);
+  float2* qab = reinterpret_cast<float2*>(smem + L::qab);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
+  const int rg = wid % kRG, qg = wid / kRG;  // 64-row group, query group
+  const int h = lane >> 5, l32 = lane & 31;
+  const int64_t q0 = (int64_t)blockIdx.y * kBQ;
+  const int nch = (a.d + kBK - 1) / kBK;
+  const int diag = a.diag;
+  filter_query_table<METRIC>(a, q0, qtab, qab, tid, kThreads);
+  const __amdgpu_buffer_rsrc_t qr = make_rsrc(a.Qh + q0 * (int64_t)a.dq, (int64_t)kBQ * a.dq * 2);
+
+  // step sequence: (tile ti, chunk c) -> stage buffer (step % 3)
+  auto tile_r0 = [&](int64_t ti) -> int64_t { return (a.tile_start + ti * a.tile_stride) * kBM; };
+  int64_t ti = blockIdx.x;
+  if (ti >= a.num_tiles) return;
+  // prologue: steps 0 and 1
+  int64_t it = ti;  // tile of the next step to issue
+  int ic = 0;       // its chunk
+  int isb = 0;      // its stage buffer
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    ring_issue<XT>(smem, a, tile_r0(it), it < a.num_tiles, ic, isb, wid, lane, qr);
+    if (++ic == nch) {
+      ic = 0;
+      it += gridDim.x;
+    }
+    isb = isb == kStages - 1 ? 0 : isb + 1;
+  }
+  int sb = 0;  // stage buffer of the current step
+  for (; ti < a.num_tiles; ti += gridDim.x) {
+    const int64_t r0 = tile_r0(ti);
+    f32x16 acc[2][kQT];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < kQT; ++u) acc[t][u] = f32x16(0.f);
+    float sq[2] = {0.f, 0.f};
+    uint32_t ovf = 0u;
+    for (int c = 0; c < nch; ++c) {
+      ring_sync<L::ndma>();
+      ring_issue<XT>(smem, a, tile_r0(it), it < a.num_tiles, ic, isb, wid, (int)opaque(lane), qr);
+      if (++ic == nch) {
+        ic = 0;
+        it += gridDim.x;
+      }
+      isb = isb == kStages - 1 ? 0 : isb + 1;
+      if (!(diag & 4)) {
+        const int ol = (int)opaque(lane);
+        ring_compute<XT>(acc, smem + sb * L::stage, rg, qg, ol & 31, ol >> 5, a.d - c * kBK, sq,
+                         ovf);
+      }
+      sb = sb == kStages - 1 ? 0 : sb + 1;
+    }
+    // row values: query-group-0 waves hold the rows' partial sums (lane halves)
+    if (qg == 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        sq[t] += __shfl_xor(sq[t], 32);
+        const uint32_t of = (ovf | __shfl_xor(ovf, 32)) >> t & 1u;
+        if (h == 0) {
+          const int lr = rg * 64 + t * 32 + l32;
+          const int64_t row = r0 + lr;
+          bool ok = row < a.n;
+          if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
+          float rv;
+          if constexpr (METRIC == 0) {
+            rv = sq[t];
+          } else if constexpr (METRIC == 1) {
+            rv = sqrtf(sq[t]);
+          } else {
+            rv = fmaxf(sqrtf(sq[t]), 1e-12f);
+          }
+          if (!(sq[t] <= 3.4e38f) || of) rv = __builtin_nanf("");
+          rinfo[lr] = ok ? rv : -1.f;
+        }
+      }
+    }
+    lds_sync();
+    if (!(diag & 2)) {
+      const int ol = (int)opaque(lane);  // keep the epilogue's lane math out of the chunk loop
+      filter_epilogue<METRIC, kQT>(acc, rinfo, qtab, qab, a, q0, r0, rg, qg, ol >> 5, ol & 31,
+                                   diag);
     }
   }
+  // drain: the ring's last DMAs (empty descriptors past the end) must land
+  // before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// f32 corpora: the register-staged kernel by default (measured faster: 8.5 vs
+// 10.1 ms for configs[2]); FX_FILTER_RING=1 selects the ring.  f16 corpora
+// always take the ring (the register kernel converts f32 rows only).
+bool filter_ring() {
+  const char* env = getenv("FX_FILTER_RING");
+  return env != nullptr && atoi(env) != 0;
+}
+
+template <typename XT>
+static int launch_ring(const FilterArgs& a, int metric, hipStream_t stream) {
+  const size_t smem = ring::Lay<XT>::total;
+  const void* fn = metric == FX_METRIC_COS ? (const void*)ring_kernel<XT, 2>
+                   : metric == FX_METRIC_IP ? (const void*)ring_kernel<XT, 1>
+                                            : (const void*)ring_kernel<XT, 0>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)ring_kernel<XT, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    (void)hipFuncSetAttribute((const void*)ring_kernel<XT, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    (void)hipFuncSetAttribute((const void*)ring_kernel<XT, 0>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr = true;
+  }
+  int cus = 0;
+  int rc = device_cus(&cus);
+  if (rc) return rc;
+  const int64_t qtiles = (a.nq + ring::kBQ - 1) / ring::kBQ;
+  int64_t bx = cus;
+  if (bx > a.num_tiles) bx = a.num_tiles;
+  for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
+    FilterArgs b = a;
+    const int64_t yn = (qtiles - y0) < 65535 ? (qtiles - y0) : 65535;
+    b.Qh = a.Qh + y0 * ring::kBQ * (int64_t)a.dq;
+    b.qinfo = a.qinfo + y0 * ring::kBQ * 4;
+    b.thr = a.thr + y0 * ring::kBQ;
+    b.count = a.count + y0 * ring::kBQ * kCountStride;
+    b.cand = a.cand + y0 * ring::kBQ * (int64_t)a.cap;
+    if (a.cand_ub) b.cand_ub = a.cand_ub + y0 * ring::kBQ * (int64_t)a.cap;
+    b.nq = a.nq - y0 * ring::kBQ;
+    void* args[] = {(void*)&b};
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(ring::kThreads),
+                                   args, smem, stream);
+    if (e != hipSuccess) {
+      set_error("ring_kernel launch: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+  }
+  return check_launch("ring_kernel");
 }
 
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.num_tiles <= 0) return FX_OK;
+  if (a.dtype == FX_DTYPE_F16) return launch_ring<_Float16>(a, metric, stream);
+  if (filter_ring()) return launch_ring<float>(a, metric, stream);
   const size_t smem = sizeof(FilterShared);
   const void* fn = metric == FX_METRIC_COS ? (const void*)filter_kernel<2>
                    : metric == FX_METRIC_IP ? (const void*)filter_kernel<1>
@@ -486,9 +814,9 @@ int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
   return check_launch("filter_kernel");
 }
 
-int filter_tile_rows() { return fBM; }
+int filter_tile_rows(int dtype) { return (dtype == FX_DTYPE_F16 || filter_ring()) ? ring::kBM : fBM; }
 int filter_query_pad() { return fBQ; }
-int filter_dq(int d) { return (d + fBK - 1) / fBK * fBK; }
+int filter_dq(int d) { return (d + 63) / 64 * 64; }  // covers both kernels' K chunks
 
 // Per query: the fp16 image scaled by 2^s (max|q| in [2^14, 2^15)), zero-padded
 // to dq halves, and the bound constants {2^-s, norm term, A, B} (see the

@@ -379,14 +379,20 @@ def test_batched_equals_unbatched(eng, monkeypatch):
 
 
 @pytest.mark.parametrize("metric", METRICS)
-@pytest.mark.parametrize("n,d,nq,k", [(100_000, 768, 40, 100), (30_011, 100, 300, 7)])
-def test_batched_filter_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq, k):
+@pytest.mark.parametrize("n,d,nq,k,ring", [
+    (100_000, 768, 40, 100, "1"),
+    (30_011, 100, 300, 7, "1"),     # d not a multiple of the 32-deep K chunk
+    (30_011, 100, 300, 7, "0"),     # the register-staged filter kernel
+    (257, 64, 9, 300, "1"),         # n < k, a single partial tile
+])
+def test_batched_filter_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq, k, ring):
     """fp16-MFMA filter + exact rescoring == the single-query f32 scan, bit for
     bit (rows and distances), and the fp32-MFMA batch kernel agrees on ids."""
     x = gpu_fill(eng, n, d, seed=21)
     q = O.fill_normal(nq, d, seed=22)
     monkeypatch.delenv("FX_BATCH", raising=False)
     monkeypatch.delenv("FX_BATCH_FILTER", raising=False)
+    monkeypatch.setenv("FX_FILTER_RING", ring)
     fd, fr = gpu_search(eng, x, q, metric, k)
     monkeypatch.setenv("FX_BATCH", "0")
     sd, sr = gpu_search(eng, x, q, metric, k)
@@ -402,7 +408,25 @@ def test_batched_filter_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq
 
 
 @pytest.mark.parametrize("metric", METRICS)
-def test_batched_filter_extreme_rows_and_queries(eng, monkeypatch, metric):
+@pytest.mark.parametrize("n,d,nq,k", [(120_000, 1536, 24, 1000), (20_003, 104, 64, 10)])
+def test_batched_f16_corpus_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq, k):
+    """fp16 columns (configs[4]'s dtype) in a batch: the LDS-DMA filter reads
+    the rows exactly; results equal the per-query f16 scan bit for bit."""
+    x = gpu_fill(eng, n, d, seed=23, dtype=torch.float16)
+    q = O.fill_normal(nq, d, seed=24).astype(np.float16).astype(np.float32)
+    monkeypatch.delenv("FX_BATCH", raising=False)
+    monkeypatch.delenv("FX_BATCH_FILTER", raising=False)
+    monkeypatch.delenv("FX_FILTER_RING", raising=False)
+    fd, fr = gpu_search(eng, x, q, metric, k)
+    monkeypatch.setenv("FX_BATCH", "0")
+    sd, sr = gpu_search(eng, x, q, metric, k)
+    np.testing.assert_array_equal(fr, sr)
+    np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
+
+
+@pytest.mark.parametrize("metric", METRICS)
+@pytest.mark.parametrize("ring", ["1", "0"])
+def test_batched_filter_extreme_rows_and_queries(eng, monkeypatch, metric, ring):
     """Rows the fp16 filter cannot bound (|x| >= 65504, inf, NaN) are forced
     through; tiny-magnitude rows and queries scaled by 2^+-60 still bound
     correctly: results equal the scan's bit for bit."""
@@ -424,6 +448,7 @@ def test_batched_filter_extreme_rows_and_queries(eng, monkeypatch, metric):
     q[3] = xh[big[12]]                     # a tiny query
     q[4] = 0.0
     monkeypatch.delenv("FX_BATCH", raising=False)
+    monkeypatch.setenv("FX_FILTER_RING", ring)
     fd, fr = gpu_search(eng, x, q, metric, k)
     monkeypatch.setenv("FX_BATCH", "0")
     sd, sr = gpu_search(eng, x, q, metric, k)

@@ -30,10 +30,12 @@ def main():
     p.add_argument("--metric", default="cosine")
     p.add_argument("--iters", type=int, default=3)
     p.add_argument("--diags", default="0,1,2,3,4,6,7")
+    p.add_argument("--dtype", default="f32", choices=["f32", "f16"])
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     eng = Engine.get(dev)
-    x = torch.empty((a.n, a.d), dtype=torch.float32, device=dev)
+    x = torch.empty((a.n, a.d), dtype=torch.float16 if a.dtype == "f16" else torch.float32,
+                    device=dev)
     eng.fill(x, seed=0)
     q = torch.empty((a.nq, a.d), dtype=torch.float32, device=dev)
     eng.fill(q, seed=1)
