@@ -37,6 +37,7 @@ for step in "$@"; do
     bench3) run bench3 900 python -u bench.py --nq 256 --metric cosine --steps 5 --warmup 1 --no-cpu-baseline ;;
     prof3) run prof3 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 -u bench.py --nq 256 --metric cosine --steps 3 --warmup 1 --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    pmc3) run pmc3 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc3 -o run --output-format csv -- python3 -u bench.py --nq 256 --metric cosine --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc -o run --output-format csv -- python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     flight1) run flight1 600 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 ;;
     flight5) run flight5 900 python -u tools/bench_flight.py --n 1000000 --d 1536 --k 1000 --metric inner_product --dtype f16 --reps 10 ;;
