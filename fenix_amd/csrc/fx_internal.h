@@ -37,6 +37,10 @@ struct ScanPlan {
   int W, L, U, cap;
   size_t qbytes, smem;
   int64_t blocks, rows_per_block, nlists;
+  // quint8 rows staged by LDS-DMA (plain contiguous scans: no mask, no row
+  // list); null when not applicable.  Same rows_per_block (its U divides it).
+  ScanKernelFn fn_dma;
+  size_t smem_dma;
 };
 
 int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool aligned, ScanPlan* p);

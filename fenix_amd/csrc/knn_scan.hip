@@ -75,6 +75,16 @@
 #define FX_Q12 1
 #endif
 
+// quint8 rows through a per-wave LDS-DMA ring (global_load_lds): rows in
+// flight cost no registers, so more of them stay in flight than the register
+// tiles allow.  Rows per lane group per tile and ring depth (tiles):
+#ifndef FX_Q8DMA_U
+#define FX_Q8DMA_U 1
+#endif
+#ifndef FX_Q8DMA_STAGES
+#define FX_Q8DMA_STAGES 3
+#endif
+
 namespace fx {
 
 // ---------------------------------------------------------------- helpers --
@@ -430,7 +440,7 @@ __device__ __forceinline__ void tile_consume(const RowTile<T, W, L, U>& t, const
 template <typename T>
 constexpr int kMinWaves = sizeof(T) == 1 ? FX_Q8_WAVES : 1;
 
-template <typename T, int W, int L, int U, int METRIC, bool PIPE>
+template <typename T, int W, int L, int U, int METRIC, bool PIPE, bool DMA = false>
 __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -484,7 +494,76 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
   int cnt = 0;
   RowTile<T, W, L, U> tA, tB;
 
-  if (PIPE && nch == 1) {
+  if constexpr (DMA) {
+    // Per-wave ring of FX_Q8DMA_STAGES tiles after the block's LDS: one
+    // global_load_lds per 16-B slot column (64 lanes x 16 B = the wave's 4U
+    // rows' slot cc), issued FX_Q8DMA_STAGES - 1 tiles ahead; the counted
+    // vmcnt leaves the later tiles in flight.  Slots past the row end read a
+    // valid dummy and are replaced by the zero-point code in registers; rows
+    // past the range are clamped to its last row (never consumed).  One pass
+    // per row (nch == 1), no mask, no row list (plan_scan / launch_scan).
+    constexpr int R = FX_Q8DMA_STAGES;
+    constexpr int kTileBytes = U * L * 1024;
+    unsigned char* ring = smem + a.qbytes + (size_t)4 * a.cap * 8 + 4 * 256 * 4 +
+                          (size_t)__builtin_amdgcn_readfirstlane(wid) * R * kTileBytes;
+    const int64_t first = lo + (int64_t)wid * 4 * U;
+    const int64_t ntile = first < c.hi ? (c.hi - first + step - 1) / step : 0;
+    using V = typename VecT<T, W>::type;
+    int slot_i = 0, slot_n = R - 1;
+#pragma unroll
+    for (int j = 0; j < R - 1; ++j) {
+        const int64_t jj = j;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          int64_t row = first + jj * step + u * 4 + c.grp;
+          if (row >= c.hi) row = c.hi - 1;
+#pragma unroll
+          for (int cc = 0; cc < L; ++cc) {
+            const int sl = cc * 16 + c.jl;
+            const void* g = reinterpret_cast<const T*>(a.X) + row * (int64_t)a.d + (sl < S ? sl : 0) * 16;
+            __builtin_amdgcn_global_load_lds(
+                g, (__attribute__((address_space(3))) void*)(ring + j * kTileBytes + (u * L + cc) * 1024),
+                16, 0, 0);
+          }
+        }
+      }
+    for (int64_t i = 0; i < ntile; ++i) {
+      {
+        const int64_t jj = i + R - 1;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          int64_t row = first + jj * step + u * 4 + c.grp;
+          if (row >= c.hi) row = c.hi - 1;
+#pragma unroll
+          for (int cc = 0; cc < L; ++cc) {
+            const int sl = cc * 16 + c.jl;
+            const void* g = reinterpret_cast<const T*>(a.X) + row * (int64_t)a.d + (sl < S ? sl : 0) * 16;
+            __builtin_amdgcn_global_load_lds(
+                g, (__attribute__((address_space(3))) void*)(ring + slot_n * kTileBytes + (u * L + cc) * 1024),
+                16, 0, 0);
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((R - 1) * U * L) : "memory");
+      RowTile<T, W, L, U> t;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        t.row[u] = first + i * step + u * 4 + c.grp;
+        t.valid[u] = t.row[u] < c.hi;
+        t.src[u] = t.row[u];
+#pragma unroll
+        for (int cc = 0; cc < L; ++cc) {
+          t.v[u][cc] = *reinterpret_cast<const V*>(ring + slot_i * kTileBytes +
+                                                   (u * L + cc) * 1024 + lane * 16);
+          if (cc * 16 + c.jl >= S) t.v[u][cc] = V((T)c.qshift);  // dequantises to 0
+        }
+      }
+      tile_consume<T, W, L, U, METRIC>(t, c, thr, cnt);
+      slot_i = slot_i == R - 1 ? 0 : slot_i + 1;
+      slot_n = slot_n == R - 1 ? 0 : slot_n + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's tail loads
+  } else if (PIPE && nch == 1) {
     int64_t it = lo + (int64_t)wid * 4 * U;
     if (it < c.hi) tile_load(tA, it, 0, c);
     for (; it < c.hi; it += 2 * step) {
@@ -615,6 +694,35 @@ static int rows_unroll(int L) {
   }
 }
 
+template <int METRIC>
+static ScanKernelFn pick_q8_dma(int L) {
+  constexpr int U = FX_Q8DMA_U;
+  switch (L) {
+    case 1: return scan_kernel<uint8_t, 16, 1, U, METRIC, true, true>;
+    case 2: return scan_kernel<uint8_t, 16, 2, U, METRIC, true, true>;
+    case 3: return scan_kernel<uint8_t, 16, 3, U, METRIC, true, true>;
+    case 4: return scan_kernel<uint8_t, 16, 4, U, METRIC, true, true>;
+    default: return nullptr;
+  }
+}
+
+static ScanKernelFn select_q8_dma_kernel(int metric, int L) {
+  if (metric == 0) return pick_q8_dma<0>(L);
+  if (metric == 1) return pick_q8_dma<1>(L);
+  return pick_q8_dma<2>(L);
+}
+
+// the DMA variants may take more than the default 64 KB of dynamic LDS
+static void q8_dma_attrs() {
+  static bool done = false;
+  if (done) return;
+  for (int m = 0; m < 3; ++m)
+    for (int L : {1, 2, 3, 4})
+      (void)hipFuncSetAttribute((const void*)select_q8_dma_kernel(m, L),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  done = true;
+}
+
 ScanKernelFn select_scan_kernel(int dtype, int metric, int W, int L) {
   if (dtype == FX_DTYPE_F32) {
     if (W == 1) {
@@ -679,6 +787,16 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
     return FX_EUNSUPPORTED;
   }
   p->fn = select_scan_kernel(dtype, metric, W, L);
+  p->fn_dma = nullptr;
+  p->smem_dma = 0;
+  if (dtype == FX_DTYPE_QU8 && W == 16 && nch == 1 && U % FX_Q8DMA_U == 0) {
+    const size_t sd = smem + (size_t)4 * FX_Q8DMA_STAGES * FX_Q8DMA_U * L * 1024;
+    const char* env = getenv("FX_Q8_DMA");
+    if (sd <= 80 * 1024 && (env == nullptr || atoi(env) != 0)) {  // >= 2 workgroups per CU
+      p->fn_dma = select_q8_dma_kernel(metric, L);
+      p->smem_dma = sd;
+    }
+  }
   p->W = W;
   p->L = L;
   p->U = U;
@@ -690,6 +808,13 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   if (rc) return rc;
   rc = kernel_occupancy((const void*)p->fn, 256, smem, &occ);
   if (rc) return rc;
+  if (p->fn_dma != nullptr) {  // one grid serves both variants: the smaller occupancy
+    q8_dma_attrs();
+    int occ2 = 0;
+    rc = kernel_occupancy((const void*)p->fn_dma, 256, p->smem_dma, &occ2);
+    if (rc) return rc;
+    if (occ2 < occ) occ = occ2;
+  }
   // Two 256-thread blocks per CU already saturate HBM with the pipelined
   // tiles (sweep in profiles/), and fewer blocks mean fewer candidate lists
   // to merge.  FX_SCAN_BLOCKS_PER_CU overrides (tuning knob, microbench).
@@ -718,6 +843,11 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
 
 int launch_scan(const ScanPlan& p, const ScanArgs& a, int64_t nq, hipStream_t stream) {
   dim3 grid((unsigned)p.blocks, (unsigned)nq);
+  if (p.fn_dma != nullptr && a.mask == nullptr && a.rows == nullptr) {
+    q8_dma_attrs();
+    hipLaunchKernelGGL(p.fn_dma, grid, dim3(256), p.smem_dma, stream, a);
+    return check_launch("scan_kernel (quint8 LDS-DMA)");
+  }
   hipLaunchKernelGGL(p.fn, grid, dim3(256), p.smem, stream, a);
   return check_launch("scan_kernel");
 }
