@@ -456,6 +456,34 @@ def test_batched_filter_extreme_rows_and_queries(eng, monkeypatch, metric, ring)
     np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
 
 
+@pytest.mark.parametrize("metric", METRICS)
+def test_batched_f16_extreme_rows_and_queries(eng, monkeypatch, metric):
+    """fp16 columns with +-inf, NaN, zero, subnormal and near-max rows, and
+    queries scaled by 2^+-40: the batched (ring) path equals the scan."""
+    n, d, k = 20_000, 64, 25
+    xh = O.fill_normal(n, d, 33).astype(np.float16)
+    rs = np.random.RandomState(6)
+    sel = rs.choice(n, 40, replace=False)
+    xh[sel[:10]] = (xh[sel[:10]].astype(np.float32) * 1e-6).astype(np.float16)  # subnormal
+    xh[sel[10:15], 3] = np.inf
+    xh[sel[15:20], 5] = -np.inf
+    xh[sel[20:25], 7] = np.nan
+    xh[sel[25:30]] = 0.0
+    xh[sel[30:40]] = (np.sign(xh[sel[30:40]].astype(np.float32)) * 60000.0).astype(np.float16)
+    x = torch.from_numpy(xh).to(eng.device)
+    q = O.fill_normal(16, d, seed=34).astype(np.float16).astype(np.float32)
+    q[0] *= 2.0 ** 40
+    q[1] *= 2.0 ** -40
+    q[2] = xh[sel[35]].astype(np.float32)  # a near-max query
+    q[3] = xh[sel[2]].astype(np.float32)   # a subnormal query
+    q[4] = 0.0
+    monkeypatch.delenv("FX_BATCH", raising=False)
+    fd, fr = gpu_search(eng, x, q, metric, k)
+    monkeypatch.setenv("FX_BATCH", "0")
+    sd, sr = gpu_search(eng, x, q, metric, k)
+    np.testing.assert_array_equal(fr, sr)
+    np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
+
 
 # ---------------------------------------------------------------- row lists
 
