@@ -117,7 +117,7 @@ static constexpr int64_t kLargeMaxK = 0x7fffffffll;
 //   last:    every row with the last threshold -> final select.
 // A query whose final candidates overflow `cap` is recomputed exactly by the
 // single-query scan (fx_knn_reduce synchronises the stream once to check).
-static constexpr int64_t kBatchMinQ = 8;
+static constexpr int64_t kBatchMinQ = 2;  // 2 queries: 6.5 ms vs 2 x 4.5 ms (10Mx768)
 static constexpr int64_t kListLen = 4096;  // candidate buffer viewed as lists
 
 struct BatchLayout {
@@ -141,7 +141,10 @@ static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool align
   if (const char* env = getenv("FX_BATCH")) {
     if (atoi(env) == 0) return false;
   }
-  if (nq < kBatchMinQ || !aligned) return false;
+  int64_t min_q = kBatchMinQ;
+  if (!use_filter()) min_q = 8;  // the fp32-MFMA kernel breaks even with scans at ~8 queries
+  if (const char* env = getenv("FX_BATCH_MIN")) min_q = atoll(env) > 1 ? atoll(env) : 2;
+  if (nq < min_q || !aligned) return false;
   // the rescoring repeats the scan's 16-B slot order: f32 rows need d % 4 == 0,
   // f16 rows d % 8 == 0 and the fp16 filter in its LDS-DMA form
   if (dtype == FX_DTYPE_F32) return d % 4 == 0;
@@ -195,7 +198,7 @@ static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, 
   off += align256(b->merge.ws_bytes);
   if (b->filter) {
     b->dq = filter_dq((int)d);
-    b->nq_pad = (nq + filter_query_pad() - 1) / filter_query_pad() * filter_query_pad();
+    b->nq_pad = (nq + filter_query_pad(nq) - 1) / filter_query_pad(nq) * filter_query_pad(nq);
     b->off_cand_ub = off;
     off += align256((size_t)nq * b->cap * 8);
     b->off_qh = off;

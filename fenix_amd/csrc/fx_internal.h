@@ -119,7 +119,7 @@ bool filter_ring();
 int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
                  uint16_t* Qh, float* qinfo, hipStream_t stream);
 int filter_tile_rows(int dtype);
-int filter_query_pad();
+int filter_query_pad(int64_t nq);
 int filter_dq(int d);
 int batch_tile_rows();
 int launch_encode(const float* dist, const int64_t* row, int64_t count, uint64_t* out,

@@ -46,7 +46,19 @@
 #include "fx_internal.h"
 #include "fx_wave.h"
 
+// This file is compiled twice: as itself (256-query tiles, namespace
+// fx::q256, plus the shared entry points) and through knn_filter_q64.hip
+// (FX_FILTER_VARIANT: 64-query tiles, namespace fx::q64) for small batches,
+// where a 256-query tile would re-read and multiply mostly padding.
+#ifndef FX_FILTER_BQ
+#define FX_FILTER_BQ 256
+#endif
+#ifndef FX_FILTER_IMPL
+#define FX_FILTER_IMPL q256
+#endif
+
 namespace fx {
+namespace FX_FILTER_IMPL {
 
 #ifndef FX_FILTER_WAVES
 #define FX_FILTER_WAVES 8   // waves per workgroup (two per SIMD)
@@ -61,10 +73,10 @@ namespace fx {
 #define FX_FILTER_BM 256
 #endif
 #ifndef FX_FILTER_BK
-#define FX_FILTER_BK 32
+#define FX_FILTER_BK (FX_FILTER_BQ >= 256 ? 32 : 64)  // >= 1 query piece per thread
 #endif
 constexpr int fBM = FX_FILTER_BM;               // corpus rows per tile
-constexpr int fBQ = 256;                        // queries per block
+constexpr int fBQ = FX_FILTER_BQ;               // queries per block
 constexpr int fBK = FX_FILTER_BK;               // K chunk (elements)
 constexpr int fLds = fBK + 8;                   // padded LDS row (halves): 16 B pad
 constexpr int fWaves = FX_FILTER_WAVES;
@@ -473,9 +485,9 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
 // reads are bank-conflict free.
 namespace ring {
 #ifndef FX_RING_WAVES
-#define FX_RING_WAVES 16  // 4 per SIMD: 64 accumulator registers per wave
+#define FX_RING_WAVES (FX_FILTER_BQ >= 256 ? 16 : 8)  // 64 or 32 accumulator registers per wave
 #endif
-constexpr int kBM = 256, kBQ = 256, kBK = 32, kStages = 3, kWaves = FX_RING_WAVES;
+constexpr int kBM = 256, kBQ = FX_FILTER_BQ, kBK = 32, kStages = 3, kWaves = FX_RING_WAVES;
 constexpr int kThreads = kWaves * 64;
 constexpr int kRG = 4;                  // 64-row groups
 constexpr int kQG = kWaves / kRG;       // query groups
@@ -486,13 +498,17 @@ struct Lay {
   static constexpr int xbytes = kBM * xrow;
   static constexpr int qbytes = kBQ * kBK * 2;
   static constexpr int stage = xbytes + qbytes;
-  static constexpr int xdma = xbytes / 1024 / kWaves;  // 1 KB DMA instructions per wave
-  static constexpr int qdma = qbytes / 1024 / kWaves;
+  // 1 KB DMA instructions per wave and stage; every wave issues the same
+  // number (the counted waits rely on it), surplus ones land in a dummy KB
+  static constexpr int xblocks = xbytes / 1024, qblocks = qbytes / 1024;
+  static constexpr int xdma = (xblocks + kWaves - 1) / kWaves;
+  static constexpr int qdma = (qblocks + kWaves - 1) / kWaves;
   static constexpr int ndma = xdma + qdma;
   static constexpr int rinfo = kStages * stage;
   static constexpr int qtab = rinfo + kBM * 4;
   static constexpr int qab = qtab + kBQ * 16;
-  static constexpr int total = qab + kBQ * 8;
+  static constexpr int dummy = qab + kBQ * 8;
+  static constexpr int total = dummy + 1024;
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr;
@@ -524,6 +540,11 @@ __device__ __forceinline__ void ring_issue(unsigned char* smem, const FilterArgs
 #pragma unroll
   for (int i = 0; i < L::xdma; ++i) {
     const int j = wid * L::xdma + i;  // 1-KB block of the stage's X image
+    if (j >= L::xblocks) {            // wave-uniform: a dummy keeps the count
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr)(smem + L::dummy), 16, 0x7fff0000u,
+                                               0, 0, 0);
+      continue;
+    }
     uint32_t voff;
     if constexpr (sizeof(XT) == 4) {  // 8 rows x 8 pieces of 16 B per block
       const int row = 8 * j + (lane >> 3);
@@ -540,6 +561,11 @@ __device__ __forceinline__ void ring_issue(unsigned char* smem, const FilterArgs
 #pragma unroll
   for (int i = 0; i < L::qdma; ++i) {
     const int j = wid * L::qdma + i;  // 16 queries x 4 pieces per block
+    if (j >= L::qblocks) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (lds_ptr)(smem + L::dummy), 16, 0x7fff0000u,
+                                               0, 0, 0);
+      continue;
+    }
     const int q = 16 * j + (lane >> 2);
     const int p = (lane & 3) ^ ((q >> 2) & 3);
     const uint32_t voff = (uint32_t)((q * a.dq + p * 8) * 2);
@@ -718,14 +744,6 @@ __global__ void __launch_bounds__(ring::kThreads, ring::kWaves / 4) ring_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// f32 corpora: the register-staged kernel by default (measured faster: 8.5 vs
-// 10.1 ms for configs[2]); FX_FILTER_RING=1 selects the ring.  f16 corpora
-// always take the ring (the register kernel converts f32 rows only).
-bool filter_ring() {
-  const char* env = getenv("FX_FILTER_RING");
-  return env != nullptr && atoi(env) != 0;
-}
-
 template <typename XT>
 static int launch_ring(const FilterArgs& a, int metric, hipStream_t stream) {
   const size_t smem = ring::Lay<XT>::total;
@@ -769,7 +787,7 @@ static int launch_ring(const FilterArgs& a, int metric, hipStream_t stream) {
   return check_launch("ring_kernel");
 }
 
-int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
+int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.num_tiles <= 0) return FX_OK;
   if (a.dtype == FX_DTYPE_F16) return launch_ring<_Float16>(a, metric, stream);
   if (filter_ring()) return launch_ring<float>(a, metric, stream);
@@ -814,9 +832,30 @@ int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
   return check_launch("filter_kernel");
 }
 
-int filter_tile_rows(int dtype) { return (dtype == FX_DTYPE_F16 || filter_ring()) ? ring::kBM : fBM; }
-int filter_query_pad() { return fBQ; }
-int filter_dq(int d) { return (d + 63) / 64 * 64; }  // covers both kernels' K chunks
+static_assert(ring::kBM == fBM, "both kernels tile 256 rows");
+}  // namespace FX_FILTER_IMPL
+
+#ifndef FX_FILTER_VARIANT
+namespace q64 {
+int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_q64.hip
+}
+
+// f32 corpora: the register-staged kernel by default (measured faster: 8.5 vs
+// 10.1 ms for configs[2]); FX_FILTER_RING=1 selects the ring.  f16 corpora
+// always take the ring (the register kernel converts f32 rows only).
+bool filter_ring() {
+  const char* env = getenv("FX_FILTER_RING");
+  return env != nullptr && atoi(env) != 0;
+}
+
+// Batches of <= 64 queries take the 64-query tiles (their Qh is padded to 64)
+int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
+  return a.nq <= 64 ? q64::launch(a, metric, stream) : q256::launch(a, metric, stream);
+}
+
+int filter_tile_rows(int) { return q256::fBM; }
+int filter_query_pad(int64_t nq) { return nq <= 64 ? 64 : 256; }
+int filter_dq(int d) { return (d + 63) / 64 * 64; }  // covers every variant's K chunk
 
 // Per query: the fp16 image scaled by 2^s (max|q| in [2^14, 2^15)), zero-padded
 // to dq halves, and the bound constants {2^-s, norm term, A, B} (see the
@@ -886,5 +925,7 @@ int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int 
                      nq, nq_pad, d, dq, metric, Qh, qinfo);
   return check_launch("qprep_kernel");
 }
+
+#endif  // FX_FILTER_VARIANT
 
 }  // namespace fx

@@ -27,7 +27,7 @@ import numpy as np
 import pyarrow as pa
 import torch
 
-from . import _lib
+from . import _lib, coalesce
 
 _PINNED_CHUNK = 256 << 20  # bytes per pinned staging buffer
 
@@ -540,6 +540,29 @@ def search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: i
                masks: Optional[Sequence[Optional[torch.Tensor]]] = None,
                counts: Optional[Sequence[Optional[int]]] = None,
                ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Exact top-k over shards that may live on several devices.
+
+    A single unfiltered query goes through the serving coalescer
+    (``fenix_amd.coalesce``): concurrent requests over the same shards run as
+    one batch (returned on the host, shape [1, k]).  Everything else, and
+    every batch, runs ``_search_all``."""
+    if (queries.shape[0] == 1 and masks is None and counts is None and coalesce.enabled()
+            and k <= _lib.load().fx_max_k()):
+        key = (tuple((id(s.data), s.data.data_ptr(), s.n, s.row_base) for s in shards), metric)
+
+        def run(qs: np.ndarray, kk: int) -> Tuple[np.ndarray, np.ndarray]:
+            d, r = _search_all(shards, torch.from_numpy(qs), metric, kk)
+            return d.cpu().numpy(), r.cpu().numpy()
+
+        d, r = coalesce.default().search(key, run, queries.cpu().numpy(), k)
+        return torch.from_numpy(d), torch.from_numpy(r)
+    return _search_all(shards, queries, metric, k, masks, counts)
+
+
+def _search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: int,
+                masks: Optional[Sequence[Optional[torch.Tensor]]] = None,
+                counts: Optional[Sequence[Optional[int]]] = None,
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Exact top-k over shards that may live on several devices.
 
     Each device's shards are searched by that device's Engine (all launches are

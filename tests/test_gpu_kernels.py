@@ -384,6 +384,9 @@ def test_batched_equals_unbatched(eng, monkeypatch):
     (30_011, 100, 300, 7, "1"),     # d not a multiple of the 32-deep K chunk
     (30_011, 100, 300, 7, "0"),     # the register-staged filter kernel
     (257, 64, 9, 300, "1"),         # n < k, a single partial tile
+    (40_000, 128, 2, 50, "0"),      # the smallest batch (64-query tiles)
+    (40_000, 128, 64, 50, "1"),     # the largest 64-query tile
+    (40_000, 128, 65, 50, "0"),     # the smallest 256-query tile
 ])
 def test_batched_filter_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq, k, ring):
     """fp16-MFMA filter + exact rescoring == the single-query f32 scan, bit for

@@ -65,15 +65,20 @@ def main() -> None:
     p.add_argument("--batch", type=int, default=1000)
     p.add_argument("--reps", type=int, default=30)
     p.add_argument("--clients", type=int, default=1, help="concurrent client processes")
+    p.add_argument("--no-coalesce", action="store_true",
+                   help="serve every request alone (FENIX_AMD_COALESCE=0)")
     p.add_argument("--client", action="store_true")
     p.add_argument("--port", type=int, default=0)
     a = p.parse_args()
     if a.client:
         return client(a)
 
+    if a.no_coalesce:
+        os.environ["FENIX_AMD_COALESCE"] = "0"
     import torch
 
     import fenix_amd
+    from fenix_amd import coalesce
     from fenix_amd.engine import Engine
 
     eng = Engine.get(torch.device("cuda", 0))
@@ -132,6 +137,8 @@ def main() -> None:
         "aggregate_searches_per_s": a.clients * a.reps / sum(
             np.sum(r["lat_ms"]) / 1e3 / a.clients for r in results) if a.clients > 1 else None,
         "wall_s_incl_client_start": wall,
+        "coalesce": coalesce.enabled(),
+        "coalesced": coalesce.describe(coalesce.default()),
     }), flush=True)
 
 
