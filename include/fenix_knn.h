@@ -104,11 +104,13 @@ int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
  * fx_knn_scan launches the scan kernels (candidates into ws); fx_knn_reduce
  * launches the merge that turns them into out_dist / out_row.  Both must be
  * given the same arguments.
- * Batched queries (nq >= 8, float32, any metric; L2 through the expansion
- * with exact rescoring of the candidates) take the MFMA path: fx_knn_scan runs
- * the sampled-threshold GEMM phases and fx_knn_reduce
- * synchronises the stream once to recompute any query whose candidates
- * overflowed (exact single-query scan), so it is not graph-capturable.
+ * Batched queries (nq >= 2, float32 rows with d % 4 == 0 or float16 rows
+ * with d % 8 == 0, 16-B aligned corpus, any metric) take the matrix-core
+ * path: fx_knn_scan runs the sampled-threshold phases of the fp16-MFMA bound
+ * filter and rescores the surviving candidates exactly, so the results are
+ * bit-identical to the single-query scan; fx_knn_reduce synchronises the
+ * stream once to recompute any query whose candidates overflowed (exact
+ * single-query scan), so it is not graph-capturable.
  */
 int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
                 const float* queries, int64_t nq, int metric, int64_t k,
