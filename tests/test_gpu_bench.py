@@ -1,0 +1,52 @@
+"""bench.py keeps the driver's output contract (one JSON line with metric,
+value, roofline, cpu_baseline ...) on small shapes of each path it reports:
+the single-query scan, the batched filter, fp16 rows and quint8 codes."""
+
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+        "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+        "roofline", "cpu_baseline"}
+
+
+def run_bench(*args: str) -> dict:
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args],
+                         capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("extra", [
+    ("--d", "768"),
+    ("--nq", "16", "--metric", "cosine"),
+    ("--dtype", "f16", "--d", "1536", "--k", "1000", "--metric", "inner_product"),
+    ("--dtype", "qu8"),
+])
+def test_bench_contract(extra):
+    rec = run_bench("--rows", "300000", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+                    *extra)
+    assert KEYS <= set(rec)
+    assert rec["n_gpus"] == 1 and rec["steps"] == 3 and rec["value"] > 0
+    roof = rec["roofline"]
+    assert roof["bound"] in ("hbm", "mfma") and roof["peak"] > 0
+    assert roof["frac"] == pytest.approx(roof["achieved"] / roof["peak"])
+    assert rec["config"]["rows_per_gpu"] == 300000
+
+
+def test_bench_cpu_baseline_fields():
+    rec = run_bench("--rows", "200000", "--steps", "2", "--warmup", "1", "--cpu-rows", "20000",
+                    "--cpu-seconds", "0.5")
+    cpu = rec["cpu_baseline"]
+    assert cpu["kind"] in ("port", "reference") and cpu["cores"] >= 1 and cpu["value"] > 0
