@@ -37,13 +37,35 @@ def big():
 
 
 @pytest.mark.parametrize("metric", ["l2", "cosine", "inner_product"])
-def test_full_corpus_vs_oracle(big, metric):
+@pytest.mark.parametrize("batched", [False, True])
+def test_full_corpus_vs_oracle(big, metric, batched):
+    """The single-query scan (one query per call) and the batched filter path
+    (both queries in one call) against the float64 oracle over all rows."""
     eng, x, q, host = big
-    gd, gr = eng.search([Shard(x, 0)], torch.from_numpy(q), _lib.METRICS[metric], K)
+    m = _lib.METRICS[metric]
+    if batched:
+        gd, gr = eng.search([Shard(x, 0)], torch.from_numpy(q), m, K)
+    else:
+        res = [eng.search([Shard(x, 0)], torch.from_numpy(q[i : i + 1]), m, K) for i in range(len(q))]
+        gd, gr = torch.cat([d for d, _ in res]), torch.cat([r for _, r in res])
     gd, gr = gd.cpu().numpy(), gr.cpu().numpy()
     od, orow = O.knn(host, q, metric, K)
     near = check_topk(gd, gr, od, orow, host[:100_000], q, metric)
     assert near <= 4, f"{near} near-tie positions"
+
+
+@pytest.mark.parametrize("metric", ["l2", "cosine", "inner_product"])
+def test_full_size_batched_equals_scans(big, metric):
+    """configs[2]: 256 queries over 10M x 768 in one batched search equal 256
+    single-query scans bit for bit (rows and f32 distances)."""
+    eng, x, _, _ = big
+    q = torch.from_numpy(O.fill_normal(256, D, seed=7))
+    m = _lib.METRICS[metric]
+    bd, br = eng.search([Shard(x, 0)], q, m, K)
+    for i in range(0, 256, 17):
+        sd, sr = eng.search([Shard(x, 0)], q[i : i + 1], m, K)
+        assert torch.equal(br[i], sr[0])
+        assert torch.equal(bd[i].view(torch.int32), sd[0].view(torch.int32))
 
 
 def test_full_size_properties(big):
