@@ -509,6 +509,17 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
     const int64_t first = lo + (int64_t)wid * 4 * U;
     const int64_t ntile = first < c.hi ? (c.hi - first + step - 1) / step : 0;
     using V = typename VecT<T, W>::type;
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef float f16v __attribute__((ext_vector_type(16)));
+    static_assert(W == 16, "the DMA path scans 16 quint8 codes per lane slot");
+    const f2 z2 = {c.qshift, c.qshift};
+    f2 qreg[L][8];  // this lane's query slots (jl, jl + 16, ...), held in registers
+#pragma unroll
+    for (int cc = 0; cc < L; ++cc) {
+      const f2* qp = reinterpret_cast<const f2*>(c.q_lds + (cc * 16 + c.jl) * W);
+#pragma unroll
+      for (int p = 0; p < 8; ++p) qreg[cc][p] = qp[p];
+    }
     int slot_i = 0, slot_n = R - 1;
 #pragma unroll
     for (int j = 0; j < R - 1; ++j) {
@@ -558,7 +569,33 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
           if (cc * 16 + c.jl >= S) t.v[u][cc] = V((T)c.qshift);  // dequantises to 0
         }
       }
-      tile_consume<T, W, L, U, METRIC>(t, c, thr, cnt);
+      // tile_accumulate's quint8 arithmetic, operation for operation (so the
+      // distances equal the register-tile path's), with the query in registers
+      float acc[U], acc2[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc[u] = acc2[u] = 0.f;
+#pragma unroll
+        for (int cc = 0; cc < L; ++cc) {
+          const f16v xf = __builtin_convertvector(t.v[u][cc], f16v);
+          f2 a2 = {0.f, 0.f}, b2 = {0.f, 0.f};
+#pragma unroll
+          for (int p = 0; p < 8; ++p) {
+            const f2 x2 = {xf[2 * p], xf[2 * p + 1]};
+            if constexpr (METRIC == 0) {
+              const f2 dd = x2 - qreg[cc][p];
+              a2 = __builtin_elementwise_fma(dd, dd, a2);
+            } else {
+              const f2 dd = x2 - z2;
+              a2 = __builtin_elementwise_fma(dd, qreg[cc][p], a2);
+              if constexpr (METRIC == 2) b2 = __builtin_elementwise_fma(dd, dd, b2);
+            }
+          }
+          acc[u] += a2.x + a2.y;
+          if constexpr (METRIC == 2) acc2[u] += b2.x + b2.y;
+        }
+      }
+      tile_finish<T, W, L, U, METRIC>(t, acc, acc2, c, thr, cnt);
       slot_i = slot_i == R - 1 ? 0 : slot_i + 1;
       slot_n = slot_n == R - 1 ? 0 : slot_n + 1;
     }
