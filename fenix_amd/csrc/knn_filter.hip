@@ -39,10 +39,13 @@
 // padded by 16 B: conflict-free ds_read_b128 fragments); the pre-scaled fp16
 // query tile (L2-resident, 393 KB for 256 x 768) is staged alongside, one
 // chunk ahead.  Per-row sums of squares and fp16-overflow flags come from the
-// same registers.  Measured (10M x 768, 256 queries, tools/filter_diag.py):
-// the X stream alone runs at 6.8 TB/s; re-reading the query tile from L2 for
-// every 256-row tile and the LDS staging cost ~1.3 ms of a ~6 ms pass, the
-// MFMAs (16 % of the fp16 peak) ~1 ms, the epilogue ~0.6 ms.
+// same registers.  Measured (10M x 768, 256 queries: 8.5 ms per batch,
+// tools/filter_diag.py switching parts off): the X stream alone runs at
+// 6.8 TB/s (4.6 ms for all phases); re-reading the query tile from L2 for
+// every 256-row tile and the LDS staging add ~1.3 ms, the MFMAs (~19 % of the
+// dense fp16 peak, not overlapped with the stream inside one workgroup per
+// CU) ~1 ms, the bound/test epilogue ~0.6 ms, the appends ~0.9 ms.  The
+// 64-query variant: 4 row groups x 2 query groups of 32, K chunks of 64.
 #include "fx_internal.h"
 #include "fx_wave.h"
 
