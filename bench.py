@@ -242,8 +242,12 @@ def main():
     # batched queries (f32): by default the fp16-MFMA bound filter + exact
     # rescoring (knn_filter.hip), one HBM-bound pass over the corpus; with
     # FX_BATCH_FILTER=0 the fp32-MFMA kernel (knn_batch.hip), MFMA-bound
-    batched = nq >= 8 and args.dtype == "f32"
-    filt = batched and os.environ.get("FX_BATCH_FILTER", "1") != "0"
+    # (fx_knn_scan takes the batched path from 2 queries, 8 without the filter:
+    # f32 with d % 4 == 0, f16 with d % 8 == 0 through the filter only)
+    filt_on = os.environ.get("FX_BATCH_FILTER", "1") != "0"
+    batched = nq >= (2 if filt_on else 8) and ((args.dtype == "f32" and d % 4 == 0)
+                                            or (args.dtype == "f16" and d % 8 == 0 and filt_on))
+    filt = batched and filt_on
     if batched and not filt:
         flops = 2.0 * n * nq * d
         roof = {
