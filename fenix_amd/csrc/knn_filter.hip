@@ -357,7 +357,11 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
   const int h = lane >> 5, l32 = lane & 31;
   const int64_t q0 = (int64_t)blockIdx.y * fBQ;
   const int nch = (a.d + fBK - 1) / fBK;
+#ifdef FX_FILTER_DIAG_BUILD
   const int diag = a.diag;
+#else
+  constexpr int diag = 0;
+#endif
 
   filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
   // (the first tile's barriers order these writes before the epilogue reads)
@@ -417,19 +421,31 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     filter_load_q(pq, ad, opaque(tid), 1, diag);
     filter_load(pf[0], ad, opaque(tid), fStages);
     __syncthreads();
-    for (int c0 = 0; c0 < nch; c0 += fStages) {
+    // One K step: multiply chunk c (LDS buffer c & 1), store chunk c + 1 from
+    // its stage p, refill p with chunk c + 1 + fStages.  The main loop runs
+    // only full steps, with no branch inside (a conditional store or load
+    // makes the waitcnt pass merge pending-load states at the join and wait
+    // for every load in flight, draining the stream each iteration).
+    auto step = [&](int c, FilterPre& p) {
+      if (!(diag & 4)) filter_compute(acc, sh, c & 1, opaque(tid));
+      if (!(diag & 16)) filter_store(p, pq, sh, (c + 1) & 1, opaque(tid), sq, ovf);
+      filter_load_q(pq, ad, opaque(tid), c + 2, diag);
+      filter_load(p, ad, opaque(tid), c + 1 + fStages);
+      __syncthreads();
+    };
+    int c = 0;
+    for (; c + fStages < nch; c += fStages) {
 #pragma unroll
-      for (int j = 0; j < fStages; ++j) {
-        const int c = c0 + j;
-        if (c >= nch) break;
-        if (!(diag & 4)) filter_compute(acc, sh, c & 1, opaque(tid));
-        if (c + 1 < nch && !(diag & 16))
-          filter_store(pf[(j + 1) % fStages], pq, sh, (c + 1) & 1, opaque(tid), sq, ovf);
-        filter_load_q(pq, ad, opaque(tid), c + 2, diag);
-        filter_load(pf[(j + 1) % fStages], ad, opaque(tid), c + 1 + fStages);
-        __syncthreads();
+      for (int j = 0; j < fStages; ++j) step(c + j, pf[(j + 1) % fStages]);
+    }
+#pragma unroll
+    for (int j = 0; j + 1 < fStages; ++j) {  // c % fStages == 0 here
+      if (c + 1 < nch) {
+        step(c, pf[(j + 1) % fStages]);
+        ++c;
       }
     }
+    if (!(diag & 4)) filter_compute(acc, sh, c & 1, opaque(tid));  // last chunk
 
     // per-row value rv from |x|^2 (the fRowLanes lanes of a row hold partials):
     // cosine max(|x|, 1e-12), IP |x|, L2 |x|^2; NaN = forced through (fp16
