@@ -49,6 +49,8 @@
 #include "fx_internal.h"
 #include "fx_wave.h"
 
+#include <type_traits>
+
 // This file is compiled twice: as itself (256-query tiles, namespace
 // fx::q256, plus the shared entry points) and through knn_filter_q64.hip
 // (FX_FILTER_VARIANT: 64-query tiles, namespace fx::q64) for small batches,
@@ -88,6 +90,7 @@ constexpr int fRG = fBM / 64;                   // 64-row groups (2 MFMA row til
 constexpr int fQG = fWaves / fRG;               // query groups
 constexpr int fQT = fBQ / fQG / 32;             // 32-query MFMA tiles per wave
 constexpr int fStages = FX_FILTER_STAGES;
+static_assert(fStages == 2, "the K loop alternates two register stages and two LDS buffers");
 constexpr int fXC = fBK / 4;                    // 16-B f32 pieces per row per chunk
 constexpr int fQC = fBK / 8;                    // 16-B f16 pieces per query per chunk
 constexpr int fXP = fBM * fXC / fThreads;       // X pieces per thread per chunk
@@ -96,6 +99,7 @@ constexpr int fRowLanes = fXC;                  // lanes sharing one row's piece
 static_assert(fQG >= 1 && fRG * fQG == fWaves && fQT >= 1, "wave grid");
 static_assert(fXP >= 1 && fQP >= 1 && fBK % 16 == 0, "staging");
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
@@ -121,56 +125,90 @@ struct FilterPreQ {  // one K chunk of the (L2-resident) query tile
 // 32-bit per-lane offsets, the chunk offset in the scalar operand.
 struct FilterAddr {
   __amdgpu_buffer_rsrc_t xr, qr;
-  int d, dq;
+  int d;
+  uint32_t xs, qs;  // byte strides between a thread's consecutive X / Q pieces
 };
 
-__device__ __forceinline__ void filter_load_q(FilterPreQ& p, const FilterAddr& ad, unsigned tid,
-                                              int c, int diag) {
+// A thread's offsets, derived once per tile from opaque(tid) (so they are not
+// hoisted and kept live across the epilogue); a piece / K step / buffer then
+// adds a wave-uniform or compile-time constant: no per-use address math in
+// the K loop (v_mul_lo_u32 is quarter rate).
+constexpr uint32_t kXB = sizeof(_Float16) * fBM * fLds;  // one LDS X buffer, bytes
+constexpr uint32_t kQB = sizeof(_Float16) * fBQ * fLds;  // one LDS Q buffer, bytes
+constexpr uint32_t kQOff = 2 * kXB;                      // FilterShared::qs
+static_assert(__builtin_offsetof(FilterShared, qs) == kQOff, "LDS layout");
+struct FilterOff {
+  uint32_t xg, qg;  // global byte offsets of piece 0 (X within the tile, Q within the query tile)
+  uint32_t xw, qw;  // LDS byte addresses of the stores of piece 0 (buffer 0)
+  uint32_t xr, qr;  // LDS byte addresses of this lane's fragment reads (buffer 0)
+  int kc;           // element offset of this lane's piece within a K chunk
+};
+
+__device__ __forceinline__ FilterOff filter_offsets(unsigned t, const FilterAddr& ad, int dq) {
+  FilterOff o;
+  o.kc = (int)(t % fXC) * 4;
+  o.xg = ((t / fXC) * (unsigned)ad.d + (t % fXC) * 4) * 4;
+  o.qg = ((t / fQC) * (unsigned)dq + (t % fQC) * 8) * 2;
+  o.xw = ((t / fXC) * fLds + (t % fXC) * 4) * 2;
+  o.qw = kQOff + ((t / fQC) * fLds + (t % fQC) * 8) * 2;
+  const unsigned lane = t & 63, wid = t >> 6;
+  const unsigned rg = wid % fRG, qg = wid / fRG, h = lane >> 5, l32 = lane & 31;
+  o.xr = ((rg * 64 + l32) * fLds + 8 * h) * 2;
+  o.qr = kQOff + ((qg * fQT * 32 + l32) * fLds + 8 * h) * 2;
+  return o;
+}
+
+template <typename T>
+__device__ __forceinline__ T& lds_at(unsigned char* smem, uint32_t off) {
+  return *reinterpret_cast<T*>(smem + off);
+}
+
+__device__ __forceinline__ void filter_load_q(FilterPreQ& p, const FilterAddr& ad,
+                                              const FilterOff& o, int c, int diag) {
 #pragma unroll
   for (int i = 0; i < fQP; ++i) {
     if (diag & 8) {
       p.q[i] = i32x4(0);
       continue;
     }
-    const uint32_t off = (((i * fThreads + tid) / fQC) * (unsigned)ad.dq + (tid % fQC) * 8) * 2;
     p.q[i] = __builtin_bit_cast(
-        i32x4, __builtin_amdgcn_raw_buffer_load_b128(ad.qr, off, c * fBK * 2, 0));
+        i32x4, __builtin_amdgcn_raw_buffer_load_b128(ad.qr, o.qg + i * ad.qs, c * fBK * 2, 0));
   }
 }
 
-__device__ __forceinline__ void filter_load(FilterPre& p, const FilterAddr& ad, unsigned tid, int c) {
+__device__ __forceinline__ void filter_load(FilterPre& p, const FilterAddr& ad, const FilterOff& o,
+                                            int c) {
   const int k0 = c * fBK;
-  const unsigned c4 = tid % fXC;                 // this lane's 16-B piece of a row chunk
-  const bool in_row = k0 + (int)c4 * 4 < ad.d;  // past the row end: an offset beyond the buffer
+  // past the row end: an offset beyond the buffer (reads zeros)
+  const uint32_t base = k0 + o.kc < ad.d ? o.xg : 0x7fff0000u;
 #pragma unroll
-  for (int i = 0; i < fXP; ++i) {
-    const uint32_t off = (((i * fThreads + tid) / fXC) * (unsigned)ad.d + c4 * 4) * 4;
+  for (int i = 0; i < fXP; ++i)
     p.x[i] = __builtin_bit_cast(
-        f32x4, __builtin_amdgcn_raw_buffer_load_b128(ad.xr, in_row ? off : 0x7fff0000u, k0 * 4,
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(ad.xr, base + i * ad.xs, k0 * 4,
                                                      2 /* nt */));
-  }
 }
 
+// Stage one chunk into LDS buffer BUF: rows to fp16 (with their sums of
+// squares, as float pairs so the packed fma reads the loaded registers
+// directly, and the max |x| for the fp16-overflow test), the query pieces as
+// they are.
+template <int BUF>
 __device__ __forceinline__ void filter_store(const FilterPre& p, const FilterPreQ& pq,
-                                             FilterShared* sh, int buf, unsigned tid,
-                                             float (&sq)[fXP], uint32_t& ovf) {
+                                             unsigned char* smem, const FilterOff& o,
+                                             f32x2 (&sq)[fXP], float (&mx)[fXP]) {
 #pragma unroll
   for (int i = 0; i < fXP; ++i) {
-    const unsigned idx = i * fThreads + tid;
     const f32x4 v = p.x[i];
-    *reinterpret_cast<f16x4*>(&sh->xs[buf][(idx / fXC) * fLds + (idx % fXC) * 4]) =
+    lds_at<f16x4>(smem, o.xw + BUF * kXB + i * (fThreads / fXC) * fLds * 2) =
         __builtin_convertvector(v, f16x4);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) sq[i] = fmaf(v[t], v[t], sq[i]);
-    // a component that rounds to an fp16 infinity (|x| >= 65520)
-    const float m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-    ovf |= (uint32_t)(m >= 65520.f) << i;
+    const f32x2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
+    sq[i] = __builtin_elementwise_fma(lo, lo, sq[i]);
+    sq[i] = __builtin_elementwise_fma(hi, hi, sq[i]);
+    mx[i] = fmaxf(mx[i], fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
   }
 #pragma unroll
-  for (int i = 0; i < fQP; ++i) {
-    const unsigned idx = i * fThreads + tid;
-    *reinterpret_cast<i32x4*>(&sh->qs[buf][(idx / fQC) * fLds + (idx % fQC) * 8]) = pq.q[i];
-  }
+  for (int i = 0; i < fQP; ++i)
+    lds_at<i32x4>(smem, o.qw + BUF * kQB + i * (fThreads / fQC) * fLds * 2) = pq.q[i];
 }
 
 // Hide a value from loop-invariant code motion: addresses derived from it are
@@ -181,19 +219,18 @@ __device__ __forceinline__ unsigned opaque(unsigned v) {
   return v;
 }
 
-__device__ __forceinline__ void filter_compute(f32x16 (&acc)[2][fQT], const FilterShared* sh,
-                                               int buf, unsigned tid) {
-  const unsigned lane = tid & 63, wid = tid >> 6;
-  const unsigned rg = wid % fRG, qg = wid / fRG, h = lane >> 5, l32 = lane & 31;
-  const _Float16* xs = sh->xs[buf] + (rg * 64 + l32) * fLds + 8 * h;
-  const _Float16* qs = sh->qs[buf] + (qg * fQT * 32 + l32) * fLds + 8 * h;
+template <int BUF>
+__device__ __forceinline__ void filter_compute(f32x16 (&acc)[2][fQT], unsigned char* smem,
+                                               const FilterOff& o) {
 #pragma unroll
   for (int s = 0; s < fBK / 16; ++s) {
     f16x8 av[2], bv[fQT];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) av[t] = *reinterpret_cast<const f16x8*>(xs + t * 32 * fLds + 16 * s);
+    for (int t = 0; t < 2; ++t)
+      av[t] = lds_at<f16x8>(smem, o.xr + BUF * kXB + (t * 32 * fLds + 16 * s) * 2);
 #pragma unroll
-    for (int u = 0; u < fQT; ++u) bv[u] = *reinterpret_cast<const f16x8*>(qs + u * 32 * fLds + 16 * s);
+    for (int u = 0; u < fQT; ++u)
+      bv[u] = lds_at<f16x8>(smem, o.qr + BUF * kQB + (u * 32 * fLds + 16 * s) * 2);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -376,10 +413,13 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int u = 0; u < fQT; ++u) acc[t][u] = f32x16(0.f);
-    float sq[fXP];
+    f32x2 sq[fXP];
+    float mx[fXP];
 #pragma unroll
-    for (int i = 0; i < fXP; ++i) sq[i] = 0.f;
-    uint32_t ovf = 0u;
+    for (int i = 0; i < fXP; ++i) {
+      sq[i] = f32x2(0.f);
+      mx[i] = 0.f;
+    }
 
     const int64_t rows = a.n - r0 < fBM ? a.n - r0 : fBM;
     FilterAddr ad;
@@ -399,64 +439,71 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
       ad.qr = __builtin_amdgcn_make_buffer_rsrc(
           reinterpret_cast<void*>(((uint64_t)qhi << 32) | qlo), 0, qnb, 0x00020000);
       ad.d = a.d;
-      ad.dq = a.dq;
+      ad.xs = (uint32_t)(fThreads / fXC) * (uint32_t)a.d * 4u;
+      ad.qs = (uint32_t)(fThreads / fQC) * (uint32_t)a.dq * 2u;
     }
+    const FilterOff o = filter_offsets(opaque(tid), ad, a.dq);
 
-    // fStages register stages: chunks c + 2 .. c + fStages of X and Q are in
-    // flight while chunk c is multiplied (stage j % fStages holds chunk j).
-    // Loads are issued unconditionally (chunks past the row end read as zeros
-    // through the descriptor bounds): a load under a branch makes the compiler
-    // wait for it where the branch joins, draining the pipeline every chunk.
-    FilterPre pf[fStages];
+    // Two register stages: chunks c + 2 and c + 3 of X are in flight while
+    // chunk c is multiplied (stage j % 2 holds chunk j), the query tile one
+    // chunk ahead.  Loads are issued unconditionally (chunks past the row end
+    // read as zeros through the descriptor bounds): a load under a branch
+    // makes the compiler wait for it where the branch joins.
+    FilterPre pf[2];
     FilterPreQ pq;
-#pragma unroll
-    for (int j = 0; j < fStages; ++j) {
-      if (j == 0) filter_load_q(pq, ad, opaque(tid), 0, diag);
-      filter_load(pf[j], ad, opaque(tid), j);
-    }
-    filter_store(pf[0], pq, sh, 0, opaque(tid), sq, ovf);
+    filter_load_q(pq, ad, o, 0, diag);
+    filter_load(pf[0], ad, o, 0);
+    filter_load(pf[1], ad, o, 1);
+    filter_store<0>(pf[0], pq, smem, o, sq, mx);
     // Q one chunk ahead, issued before the X load of the same step: vmcnt
     // retires loads in issue order, so waiting for Q(c + 1) at step c waits
     // for X(c + 1) (needed there anyway) and nothing issued later.
-    filter_load_q(pq, ad, opaque(tid), 1, diag);
-    filter_load(pf[0], ad, opaque(tid), fStages);
+    filter_load_q(pq, ad, o, 1, diag);
+    filter_load(pf[0], ad, o, 2);
     __syncthreads();
-    // One K step: multiply chunk c (LDS buffer c & 1), store chunk c + 1 from
-    // its stage p, refill p with chunk c + 1 + fStages.  The main loop runs
-    // only full steps, with no branch inside (a conditional store or load
-    // makes the waitcnt pass merge pending-load states at the join and wait
-    // for every load in flight, draining the stream each iteration).
-    auto step = [&](int c, FilterPre& p) {
-      if (!(diag & 4)) filter_compute(acc, sh, c & 1, opaque(tid));
-      if (!(diag & 16)) filter_store(p, pq, sh, (c + 1) & 1, opaque(tid), sq, ovf);
-      filter_load_q(pq, ad, opaque(tid), c + 2, diag);
-      filter_load(p, ad, opaque(tid), c + 1 + fStages);
+    // One K step: multiply chunk c (LDS buffer c & 1 = B), store chunk c + 1
+    // from its stage p into the other buffer, refill p with chunk c + 3.  The
+    // main loop runs only full steps, with no branch inside (a conditional
+    // store or load makes the waitcnt pass merge pending-load states at the
+    // join and wait for every load in flight, draining the stream).
+    auto step = [&](int c, FilterPre& p, auto buf) {
+      constexpr int B = decltype(buf)::value;
+      if (!(diag & 4)) filter_compute<B>(acc, smem, o);
+      if (!(diag & 16)) filter_store<B ^ 1>(p, pq, smem, o, sq, mx);
+      filter_load_q(pq, ad, o, c + 2, diag);
+      filter_load(p, ad, o, c + 3);
       __syncthreads();
     };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
     int c = 0;
-    for (; c + fStages < nch; c += fStages) {
-#pragma unroll
-      for (int j = 0; j < fStages; ++j) step(c + j, pf[(j + 1) % fStages]);
+    for (; c + 2 < nch; c += 2) {
+      step(c, pf[1], B0{});
+      step(c + 1, pf[0], B1{});
     }
-#pragma unroll
-    for (int j = 0; j + 1 < fStages; ++j) {  // c % fStages == 0 here
-      if (c + 1 < nch) {
-        step(c, pf[(j + 1) % fStages]);
-        ++c;
-      }
-    }
-    if (!(diag & 4)) filter_compute(acc, sh, c & 1, opaque(tid));  // last chunk
+    // the last one or two chunks (c is even: chunk c sits in buffer 0, chunk
+    // c + 1, if any, in stage 1); one-sided branches only, so the
+    // accumulators need no copies at a join
+    const bool two = c + 1 < nch;
+    if (two && !(diag & 16)) filter_store<1>(pf[1], pq, smem, o, sq, mx);
+    __syncthreads();
+    if (!(diag & 4)) filter_compute<0>(acc, smem, o);
+    if (two && !(diag & 4)) filter_compute<1>(acc, smem, o);
 
     // per-row value rv from |x|^2 (the fRowLanes lanes of a row hold partials):
     // cosine max(|x|, 1e-12), IP |x|, L2 |x|^2; NaN = forced through (fp16
-    // overflow, non-finite); -1 = skipped (past n or masked out)
+    // overflow: a component >= 65520; non-finite); -1 = skipped (past n or
+    // masked out)
+    float sqs[fXP];
 #pragma unroll
     for (int i = 0; i < fXP; ++i) {
+      sqs[i] = sq[i][0] + sq[i][1];
 #pragma unroll
-      for (int m = 1; m < fRowLanes; m <<= 1) sq[i] += __shfl_xor(sq[i], m);
+      for (int m = 1; m < fRowLanes; m <<= 1) {
+        sqs[i] += __shfl_xor(sqs[i], m);
+        mx[i] = fmaxf(mx[i], __shfl_xor(mx[i], m));
+      }
     }
-#pragma unroll
-    for (int m = 1; m < fRowLanes; m <<= 1) ovf |= __shfl_xor(ovf, m);
 #pragma unroll
     for (int i = 0; i < fXP; ++i) {
       if (tid % fRowLanes == 0) {
@@ -466,13 +513,13 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
         if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
         float rv;
         if constexpr (METRIC == 0) {
-          rv = sq[i];
+          rv = sqs[i];
         } else if constexpr (METRIC == 1) {
-          rv = sqrtf(sq[i]);
+          rv = sqrtf(sqs[i]);
         } else {
-          rv = fmaxf(sqrtf(sq[i]), 1e-12f);
+          rv = fmaxf(sqrtf(sqs[i]), 1e-12f);
         }
-        if (!(sq[i] <= 3.4e38f) || ((ovf >> i) & 1u)) rv = __builtin_nanf("");
+        if (!(sqs[i] <= 3.4e38f) || mx[i] >= 65520.f) rv = __builtin_nanf("");
         sh->rinfo[lr] = ok ? rv : -1.f;
       }
     }
