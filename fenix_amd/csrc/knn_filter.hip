@@ -898,7 +898,6 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   return check_launch("filter_kernel");
 }
 
-static_assert(ring::kBM == fBM, "both kernels tile 256 rows");
 }  // namespace FX_FILTER_IMPL
 
 #ifndef FX_FILTER_VARIANT
@@ -919,7 +918,12 @@ int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
   return a.nq <= 64 ? q64::launch(a, metric, stream) : q256::launch(a, metric, stream);
 }
 
-int filter_tile_rows(int) { return q256::fBM; }
+// rows per tile of the kernel launch_filter picks for the dtype (the 64-query
+// variant tiles rows like the 256-query one)
+int filter_tile_rows(int dtype) {
+  return dtype == FX_DTYPE_F16 || filter_ring() ? q256::ring::kBM : q256::fBM;
+}
+
 int filter_query_pad(int64_t nq) { return nq <= 64 ? 64 : 256; }
 int filter_dq(int d) { return (d + 63) / 64 * 64; }  // covers every variant's K chunk
 

@@ -1,14 +1,15 @@
 #!/bin/bash
-# Same-box A/B of two builds of the library (box-to-box HBM variance is a few
-# per cent, larger than most kernel changes).  Build the baseline first:
+# Same-box A/B of builds of the library (box-to-box HBM variance is a few per
+# cent, larger than most kernel changes).  Build the variants first, e.g.
 #   git stash && make -C fenix_amd/csrc BUILD=build_old OUT=../lib/libfenix_knn_old.so && git stash pop
-# then: gpurun -- 'bash tools/ab_libs.sh [bench.py args...]'
+# then: gpurun -- 'LIBS="new old" bash tools/ab_libs.sh [bench.py args...]'
+# ("new" is fenix_amd/lib/libfenix_knn.so, NAME is fenix_amd/lib/libfenix_knn_NAME.so)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 ARGS=${*:-"--nq 256 --metric cosine"}
 for i in 1 2; do
-  for v in new old; do
-    if [ $v = old ]; then export FENIX_AMD_LIB=$PWD/fenix_amd/lib/libfenix_knn_old.so; else unset FENIX_AMD_LIB; fi
+  for v in ${LIBS:-new old}; do
+    if [ "$v" = new ]; then unset FENIX_AMD_LIB; else export FENIX_AMD_LIB=$PWD/fenix_amd/lib/libfenix_knn_$v.so; fi
     log=gpurun_out/ab_$v.$i.log
     timeout -k 10 200 python -u bench.py $ARGS --steps 10 --warmup 2 --no-cpu-baseline > $log 2>&1 || exit 1
     python -c "
