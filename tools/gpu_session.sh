@@ -31,6 +31,9 @@ for step in "$@"; do
     profq8) run profq8 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profq8 -o run --output-format csv -- python3 -u bench.py --dtype qu8 --steps 10 --warmup 2 --no-cpu-baseline ;;
     testbatch) run pytest_batch 900 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k batch -p no:cacheprovider ;;
     bench3l2) run bench3l2 900 python -u bench.py --nq 256 --metric l2 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    bench3ip) run bench3ip 900 python -u bench.py --nq 256 --metric inner_product --steps 5 --warmup 1 --no-cpu-baseline ;;
+    ktrace3) run ktrace3 600 rocprofv3 --kernel-trace -d gpurun_out/ktrace3 -o run --output-format csv -- python3 -u bench.py --nq 256 --metric cosine --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmcsq3) run pmcsq3 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d gpurun_out/pmcsq -o run --output-format csv -- python3 -u bench.py --nq 256 --metric cosine --steps 1 --warmup 0 --no-cpu-baseline ;;
     testk) run pytest_kernels 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_fullsize.py -m gpu -q -x -p no:cacheprovider ;;
     testsall) run pytest_gpu 1500 python -u -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python -u bench.py ;;
