@@ -4,7 +4,7 @@ The reference serves every ``Flight.search`` as its own ``do_exchange`` call
 (src/fenix/flight.py:62-77 -> io.index.call), and so does this engine: one
 exact scan of the whole column per query.  On a large resident column that
 scan is HBM-bound (10M x 768 f32: 4.4 ms), while a batch of queries costs
-about one pass over the column through the fp16 filter (256 queries: 8.5 ms,
+about one pass over the column through the fp16 filter (256 queries: 8.2 ms,
 DESIGN.md §3.6).  So when requests arrive while the device is busy, they are
 worth running together.
 
