@@ -146,7 +146,7 @@ static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool align
   if (const char* env = getenv("FX_BATCH_MIN")) min_q = atoll(env) > 1 ? atoll(env) : 2;
   if (nq < min_q || !aligned) return false;
   // the rescoring repeats the scan's 16-B slot order: f32 rows need d % 4 == 0,
-  // f16 rows d % 8 == 0 and the fp16 filter in its LDS-DMA form
+  // f16 rows d % 8 == 0 (and the fp16 filter: the fp32-MFMA kernel reads f32 only)
   if (dtype == FX_DTYPE_F32) return d % 4 == 0;
   return dtype == FX_DTYPE_F16 && d % 8 == 0 && use_filter();
 }

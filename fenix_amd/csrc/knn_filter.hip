@@ -91,13 +91,19 @@ constexpr int fQG = fWaves / fRG;               // query groups
 constexpr int fQT = fBQ / fQG / 32;             // 32-query MFMA tiles per wave
 constexpr int fStages = FX_FILTER_STAGES;
 static_assert(fStages == 2, "the K loop alternates two register stages and two LDS buffers");
-constexpr int fXC = fBK / 4;                    // 16-B f32 pieces per row per chunk
 constexpr int fQC = fBK / 8;                    // 16-B f16 pieces per query per chunk
-constexpr int fXP = fBM * fXC / fThreads;       // X pieces per thread per chunk
 constexpr int fQP = fBQ * fQC / fThreads;       // Q pieces per thread per chunk
-constexpr int fRowLanes = fXC;                  // lanes sharing one row's pieces
+// Rows of type XT (float or _Float16) come in 16-B pieces of E elements;
+// C pieces per row per chunk (the lanes sharing a row), P per thread.
+template <typename XT>
+struct XPiece {
+  static constexpr int E = 16 / (int)sizeof(XT);
+  static constexpr int C = fBK / E;
+  static constexpr int P = fBM * C / fThreads;
+  static_assert(P >= 1 && fThreads % C == 0, "row staging");
+};
 static_assert(fQG >= 1 && fRG * fQG == fWaves && fQT >= 1, "wave grid");
-static_assert(fXP >= 1 && fQP >= 1 && fBK % 16 == 0, "staging");
+static_assert(fQP >= 1 && fBK % 16 == 0, "staging");
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -114,8 +120,9 @@ struct FilterShared {
   float2 qab[fBQ];   // per query: pass iff product >= a * row value + b
 };
 
+template <typename XT>
 struct FilterPre {  // one K chunk of X rows in flight
-  f32x4 x[fXP];
+  i32x4 x[XPiece<XT>::P];
 };
 struct FilterPreQ {  // one K chunk of the (L2-resident) query tile
   i32x4 q[fQP];
@@ -144,12 +151,14 @@ struct FilterOff {
   int kc;           // element offset of this lane's piece within a K chunk
 };
 
+template <typename XT>
 __device__ __forceinline__ FilterOff filter_offsets(unsigned t, const FilterAddr& ad, int dq) {
+  using X = XPiece<XT>;
   FilterOff o;
-  o.kc = (int)(t % fXC) * 4;
-  o.xg = ((t / fXC) * (unsigned)ad.d + (t % fXC) * 4) * 4;
+  o.kc = (int)(t % X::C) * X::E;
+  o.xg = ((t / X::C) * (unsigned)ad.d + (t % X::C) * X::E) * (unsigned)sizeof(XT);
   o.qg = ((t / fQC) * (unsigned)dq + (t % fQC) * 8) * 2;
-  o.xw = ((t / fXC) * fLds + (t % fXC) * 4) * 2;
+  o.xw = ((t / X::C) * fLds + (t % X::C) * X::E) * 2;
   o.qw = kQOff + ((t / fQC) * fLds + (t % fQC) * 8) * 2;
   const unsigned lane = t & 63, wid = t >> 6;
   const unsigned rg = wid % fRG, qg = wid / fRG, h = lane >> 5, l32 = lane & 31;
@@ -176,35 +185,50 @@ __device__ __forceinline__ void filter_load_q(FilterPreQ& p, const FilterAddr& a
   }
 }
 
-__device__ __forceinline__ void filter_load(FilterPre& p, const FilterAddr& ad, const FilterOff& o,
-                                            int c) {
+template <typename XT>
+__device__ __forceinline__ void filter_load(FilterPre<XT>& p, const FilterAddr& ad,
+                                            const FilterOff& o, int c) {
   const int k0 = c * fBK;
   // past the row end: an offset beyond the buffer (reads zeros)
   const uint32_t base = k0 + o.kc < ad.d ? o.xg : 0x7fff0000u;
 #pragma unroll
-  for (int i = 0; i < fXP; ++i)
+  for (int i = 0; i < XPiece<XT>::P; ++i)
     p.x[i] = __builtin_bit_cast(
-        f32x4, __builtin_amdgcn_raw_buffer_load_b128(ad.xr, base + i * ad.xs, k0 * 4,
-                                                     2 /* nt */));
+        i32x4, __builtin_amdgcn_raw_buffer_load_b128(ad.xr, base + i * ad.xs,
+                                                     k0 * (int)sizeof(XT), 2 /* nt */));
 }
 
-// Stage one chunk into LDS buffer BUF: rows to fp16 (with their sums of
+// Stage one chunk into LDS buffer BUF: f32 rows to fp16 (with their sums of
 // squares, as float pairs so the packed fma reads the loaded registers
-// directly, and the max |x| for the fp16-overflow test), the query pieces as
-// they are.
-template <int BUF>
-__device__ __forceinline__ void filter_store(const FilterPre& p, const FilterPreQ& pq,
+// directly, and the max |x| for the fp16-overflow test), fp16 rows as they
+// are (sums of squares of the exact f32 values; an fp16 row cannot overflow,
+// an infinity or NaN shows in the sum), the query pieces as they are.
+template <typename XT, int BUF>
+__device__ __forceinline__ void filter_store(const FilterPre<XT>& p, const FilterPreQ& pq,
                                              unsigned char* smem, const FilterOff& o,
-                                             f32x2 (&sq)[fXP], float (&mx)[fXP]) {
+                                             f32x2 (&sq)[XPiece<XT>::P],
+                                             float (&mx)[XPiece<XT>::P]) {
+  using X = XPiece<XT>;
 #pragma unroll
-  for (int i = 0; i < fXP; ++i) {
-    const f32x4 v = p.x[i];
-    lds_at<f16x4>(smem, o.xw + BUF * kXB + i * (fThreads / fXC) * fLds * 2) =
-        __builtin_convertvector(v, f16x4);
-    const f32x2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
-    sq[i] = __builtin_elementwise_fma(lo, lo, sq[i]);
-    sq[i] = __builtin_elementwise_fma(hi, hi, sq[i]);
-    mx[i] = fmaxf(mx[i], fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  for (int i = 0; i < X::P; ++i) {
+    const uint32_t at = o.xw + BUF * kXB + i * (fThreads / X::C) * fLds * 2;
+    if constexpr (sizeof(XT) == 4) {
+      const f32x4 v = __builtin_bit_cast(f32x4, p.x[i]);
+      lds_at<f16x4>(smem, at) = __builtin_convertvector(v, f16x4);
+      const f32x2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
+      sq[i] = __builtin_elementwise_fma(lo, lo, sq[i]);
+      sq[i] = __builtin_elementwise_fma(hi, hi, sq[i]);
+      mx[i] = fmaxf(mx[i],
+                    fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    } else {
+      lds_at<i32x4>(smem, at) = p.x[i];
+      const f16x8 h = __builtin_bit_cast(f16x8, p.x[i]);
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const f32x2 v = {(float)h[e], (float)h[e + 1]};
+        sq[i] = __builtin_elementwise_fma(v, v, sq[i]);
+      }
+    }
   }
 #pragma unroll
   for (int i = 0; i < fQP; ++i)
@@ -385,8 +409,9 @@ __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], cons
     }
 }
 
-template <int METRIC>
+template <typename XT, int METRIC>
 __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_kernel(FilterArgs a) {
+  using X = XPiece<XT>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   FilterShared* sh = reinterpret_cast<FilterShared*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -413,10 +438,10 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int u = 0; u < fQT; ++u) acc[t][u] = f32x16(0.f);
-    f32x2 sq[fXP];
-    float mx[fXP];
+    f32x2 sq[X::P];
+    float mx[X::P];
 #pragma unroll
-    for (int i = 0; i < fXP; ++i) {
+    for (int i = 0; i < X::P; ++i) {
       sq[i] = f32x2(0.f);
       mx[i] = 0.f;
     }
@@ -424,11 +449,11 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     const int64_t rows = a.n - r0 < fBM ? a.n - r0 : fBM;
     FilterAddr ad;
     {
-      const float* xb = reinterpret_cast<const float*>(a.X) + r0 * (int64_t)a.d;
+      const XT* xb = reinterpret_cast<const XT*>(a.X) + r0 * (int64_t)a.d;
       const uint64_t xp = reinterpret_cast<uint64_t>(xb);
       const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xp);
       const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xp >> 32));
-      const int nb = __builtin_amdgcn_readfirstlane((int)(rows * a.d * 4));
+      const int nb = __builtin_amdgcn_readfirstlane((int)(rows * a.d * (int64_t)sizeof(XT)));
       ad.xr = __builtin_amdgcn_make_buffer_rsrc(
           reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
       const uint16_t* qb = a.Qh + q0 * (int64_t)a.dq;
@@ -439,22 +464,22 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
       ad.qr = __builtin_amdgcn_make_buffer_rsrc(
           reinterpret_cast<void*>(((uint64_t)qhi << 32) | qlo), 0, qnb, 0x00020000);
       ad.d = a.d;
-      ad.xs = (uint32_t)(fThreads / fXC) * (uint32_t)a.d * 4u;
+      ad.xs = (uint32_t)(fThreads / X::C) * (uint32_t)a.d * (uint32_t)sizeof(XT);
       ad.qs = (uint32_t)(fThreads / fQC) * (uint32_t)a.dq * 2u;
     }
-    const FilterOff o = filter_offsets(opaque(tid), ad, a.dq);
+    const FilterOff o = filter_offsets<XT>(opaque(tid), ad, a.dq);
 
     // Two register stages: chunks c + 2 and c + 3 of X are in flight while
     // chunk c is multiplied (stage j % 2 holds chunk j), the query tile one
     // chunk ahead.  Loads are issued unconditionally (chunks past the row end
     // read as zeros through the descriptor bounds): a load under a branch
     // makes the compiler wait for it where the branch joins.
-    FilterPre pf[2];
+    FilterPre<XT> pf[2];
     FilterPreQ pq;
     filter_load_q(pq, ad, o, 0, diag);
     filter_load(pf[0], ad, o, 0);
     filter_load(pf[1], ad, o, 1);
-    filter_store<0>(pf[0], pq, smem, o, sq, mx);
+    filter_store<XT, 0>(pf[0], pq, smem, o, sq, mx);
     // Q one chunk ahead, issued before the X load of the same step: vmcnt
     // retires loads in issue order, so waiting for Q(c + 1) at step c waits
     // for X(c + 1) (needed there anyway) and nothing issued later.
@@ -466,10 +491,10 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     // main loop runs only full steps, with no branch inside (a conditional
     // store or load makes the waitcnt pass merge pending-load states at the
     // join and wait for every load in flight, draining the stream).
-    auto step = [&](int c, FilterPre& p, auto buf) {
+    auto step = [&](int c, FilterPre<XT>& p, auto buf) {
       constexpr int B = decltype(buf)::value;
       if (!(diag & 4)) filter_compute<B>(acc, smem, o);
-      if (!(diag & 16)) filter_store<B ^ 1>(p, pq, smem, o, sq, mx);
+      if (!(diag & 16)) filter_store<XT, B ^ 1>(p, pq, smem, o, sq, mx);
       filter_load_q(pq, ad, o, c + 2, diag);
       filter_load(p, ad, o, c + 3);
       __syncthreads();
@@ -485,7 +510,7 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     // c + 1, if any, in stage 1); one-sided branches only, so the
     // accumulators need no copies at a join
     const bool two = c + 1 < nch;
-    if (two && !(diag & 16)) filter_store<1>(pf[1], pq, smem, o, sq, mx);
+    if (two && !(diag & 16)) filter_store<XT, 1>(pf[1], pq, smem, o, sq, mx);
     __syncthreads();
     if (!(diag & 4)) filter_compute<0>(acc, smem, o);
     if (two && !(diag & 4)) filter_compute<1>(acc, smem, o);
@@ -494,20 +519,20 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     // cosine max(|x|, 1e-12), IP |x|, L2 |x|^2; NaN = forced through (fp16
     // overflow: a component >= 65520; non-finite); -1 = skipped (past n or
     // masked out)
-    float sqs[fXP];
+    float sqs[X::P];
 #pragma unroll
-    for (int i = 0; i < fXP; ++i) {
+    for (int i = 0; i < X::P; ++i) {
       sqs[i] = sq[i][0] + sq[i][1];
 #pragma unroll
-      for (int m = 1; m < fRowLanes; m <<= 1) {
+      for (int m = 1; m < X::C; m <<= 1) {
         sqs[i] += __shfl_xor(sqs[i], m);
         mx[i] = fmaxf(mx[i], __shfl_xor(mx[i], m));
       }
     }
 #pragma unroll
-    for (int i = 0; i < fXP; ++i) {
-      if (tid % fRowLanes == 0) {
-        const int lr = (i * fThreads + tid) / fXC;
+    for (int i = 0; i < X::P; ++i) {
+      if (tid % X::C == 0) {
+        const int lr = (i * fThreads + tid) / X::C;
         const int64_t row = r0 + lr;
         bool ok = row < a.n;
         if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
@@ -855,20 +880,21 @@ static int launch_ring(const FilterArgs& a, int metric, hipStream_t stream) {
 
 int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.num_tiles <= 0) return FX_OK;
-  if (a.dtype == FX_DTYPE_F16) return launch_ring<_Float16>(a, metric, stream);
-  if (filter_ring()) return launch_ring<float>(a, metric, stream);
+  const bool f16 = a.dtype == FX_DTYPE_F16;
+  if (filter_ring()) return f16 ? launch_ring<_Float16>(a, metric, stream)
+                                : launch_ring<float>(a, metric, stream);
   const size_t smem = sizeof(FilterShared);
-  const void* fn = metric == FX_METRIC_COS ? (const void*)filter_kernel<2>
-                   : metric == FX_METRIC_IP ? (const void*)filter_kernel<1>
-                                            : (const void*)filter_kernel<0>;
+  const void* fns[2][3] = {
+      {(const void*)filter_kernel<float, 0>, (const void*)filter_kernel<float, 1>,
+       (const void*)filter_kernel<float, 2>},
+      {(const void*)filter_kernel<_Float16, 0>, (const void*)filter_kernel<_Float16, 1>,
+       (const void*)filter_kernel<_Float16, 2>}};
+  const void* fn = fns[f16][metric == FX_METRIC_COS ? 2 : metric == FX_METRIC_IP ? 1 : 0];
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)filter_kernel<2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    (void)hipFuncSetAttribute((const void*)filter_kernel<1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    (void)hipFuncSetAttribute((const void*)filter_kernel<0>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    for (auto& row : fns)
+      for (const void* f : row)
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
   int cus = 0;
@@ -905,9 +931,9 @@ namespace q64 {
 int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_q64.hip
 }
 
-// f32 corpora: the register-staged kernel by default (measured faster: 8.5 vs
-// 10.1 ms for configs[2]); FX_FILTER_RING=1 selects the ring.  f16 corpora
-// always take the ring (the register kernel converts f32 rows only).
+// The register-staged kernel by default (measured faster for both row types:
+// 8.5 vs 10.1 ms for configs[2]; see DESIGN.md for fp16); FX_FILTER_RING=1
+// selects the LDS-DMA ring.
 bool filter_ring() {
   const char* env = getenv("FX_FILTER_RING");
   return env != nullptr && atoi(env) != 0;

@@ -411,15 +411,18 @@ def test_batched_filter_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq
 
 
 @pytest.mark.parametrize("metric", METRICS)
-@pytest.mark.parametrize("n,d,nq,k", [(120_000, 1536, 24, 1000), (20_003, 104, 64, 10)])
-def test_batched_f16_corpus_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq, k):
-    """fp16 columns (configs[4]'s dtype) in a batch: the LDS-DMA filter reads
-    the rows exactly; results equal the per-query f16 scan bit for bit."""
+@pytest.mark.parametrize("n,d,nq,k", [(120_000, 1536, 24, 1000), (20_003, 104, 64, 10),
+                                      (50_000, 768, 256, 100)])
+@pytest.mark.parametrize("ring", ["0", "1"])
+def test_batched_f16_corpus_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq, k, ring):
+    """fp16 columns (configs[4]'s dtype) in a batch: the filter (register-
+    staged kernel, or the LDS-DMA ring) reads the rows exactly; results equal
+    the per-query f16 scan bit for bit."""
     x = gpu_fill(eng, n, d, seed=23, dtype=torch.float16)
     q = O.fill_normal(nq, d, seed=24).astype(np.float16).astype(np.float32)
     monkeypatch.delenv("FX_BATCH", raising=False)
     monkeypatch.delenv("FX_BATCH_FILTER", raising=False)
-    monkeypatch.delenv("FX_FILTER_RING", raising=False)
+    monkeypatch.setenv("FX_FILTER_RING", ring)
     fd, fr = gpu_search(eng, x, q, metric, k)
     monkeypatch.setenv("FX_BATCH", "0")
     sd, sr = gpu_search(eng, x, q, metric, k)
@@ -460,9 +463,11 @@ def test_batched_filter_extreme_rows_and_queries(eng, monkeypatch, metric, ring)
 
 
 @pytest.mark.parametrize("metric", METRICS)
-def test_batched_f16_extreme_rows_and_queries(eng, monkeypatch, metric):
+@pytest.mark.parametrize("ring", ["0", "1"])
+def test_batched_f16_extreme_rows_and_queries(eng, monkeypatch, metric, ring):
     """fp16 columns with +-inf, NaN, zero, subnormal and near-max rows, and
-    queries scaled by 2^+-40: the batched (ring) path equals the scan."""
+    queries scaled by 2^+-40: the batched path (either filter kernel) equals
+    the scan."""
     n, d, k = 20_000, 64, 25
     xh = O.fill_normal(n, d, 33).astype(np.float16)
     rs = np.random.RandomState(6)
@@ -481,6 +486,7 @@ def test_batched_f16_extreme_rows_and_queries(eng, monkeypatch, metric):
     q[3] = xh[sel[2]].astype(np.float32)   # a subnormal query
     q[4] = 0.0
     monkeypatch.delenv("FX_BATCH", raising=False)
+    monkeypatch.setenv("FX_FILTER_RING", ring)
     fd, fr = gpu_search(eng, x, q, metric, k)
     monkeypatch.setenv("FX_BATCH", "0")
     sd, sr = gpu_search(eng, x, q, metric, k)
