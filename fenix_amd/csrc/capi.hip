@@ -334,6 +334,7 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, int64_t
     a.row_base = row_base;
     a.Qh = qh;
     a.dq = b.dq;
+    a.qstride = b.nq_pad;
     a.qinfo = qinfo;
     a.nq = nq;
     a.mask = mask;

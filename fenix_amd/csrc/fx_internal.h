@@ -93,13 +93,15 @@ int launch_rescore(const void* X, int dtype, int64_t n, int d, int64_t row_base,
 // Batched filter on the fp16 matrix cores (knn_filter.hip): appends every
 // (row, query) whose rigorous lower bound reaches the query's threshold.
 struct FilterArgs {
-  const void* X;          // [n][d] corpus shard (f32; f16 with the ring kernel)
+  const void* X;          // [n][d] corpus shard (f32 or f16)
   int dtype;              // FX_DTYPE_F32 / FX_DTYPE_F16
   int64_t n;
   int d;
   int64_t row_base;
-  const uint16_t* Qh;     // [nq_pad][dq] fp16 queries, scaled by a power of two
-  int dq;
+  const uint16_t* Qh;     // fp16 queries scaled by a power of two, in blocks of 32
+                          // components: (q, k) at ((k / 32) * qstride + q) * 32 + k % 32
+  int dq;                 // components per query, padded (a multiple of 64)
+  int64_t qstride;        // queries per block row (nq_pad)
   const float* qinfo;     // [nq][4] {1/scale, norm term, A, B}
   int64_t nq;
   const uint32_t* mask;
@@ -113,8 +115,8 @@ struct FilterArgs {
                           // 4 no MFMA, 8 no query loads, 16 no LDS stores
 };
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream);
-// the LDS-DMA ring variant (knn_filter.hip ring_kernel): always for f16 rows,
-// for f32 rows with FX_FILTER_RING=1 (the register-staged kernel otherwise)
+// the LDS-DMA ring variant (knn_filter.hip ring_kernel) with FX_FILTER_RING=1
+// (the register-staged kernel otherwise)
 bool filter_ring();
 int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
                  uint16_t* Qh, float* qinfo, hipStream_t stream);

@@ -132,8 +132,9 @@ struct FilterPreQ {  // one K chunk of the (L2-resident) query tile
 // 32-bit per-lane offsets, the chunk offset in the scalar operand.
 struct FilterAddr {
   __amdgpu_buffer_rsrc_t xr, qr;
-  int d;
+  int d, dq;
   uint32_t xs, qs;  // byte strides between a thread's consecutive X / Q pieces
+  uint32_t qb;      // byte stride between blocks of 32 query components
 };
 
 // A thread's offsets, derived once per tile from opaque(tid) (so they are not
@@ -152,12 +153,13 @@ struct FilterOff {
 };
 
 template <typename XT>
-__device__ __forceinline__ FilterOff filter_offsets(unsigned t, const FilterAddr& ad, int dq) {
+__device__ __forceinline__ FilterOff filter_offsets(unsigned t, const FilterAddr& ad) {
   using X = XPiece<XT>;
   FilterOff o;
   o.kc = (int)(t % X::C) * X::E;
   o.xg = ((t / X::C) * (unsigned)ad.d + (t % X::C) * X::E) * (unsigned)sizeof(XT);
-  o.qg = ((t / fQC) * (unsigned)dq + (t % fQC) * 8) * 2;
+  // query piece p = t % fQC of a chunk: block p / 4, 16 B p % 4 of the query's 64
+  o.qg = (t / fQC) * 64 + (t % fQC) % 4 * 16 + (t % fQC) / 4 * ad.qb;
   o.xw = ((t / X::C) * fLds + (t % X::C) * X::E) * 2;
   o.qw = kQOff + ((t / fQC) * fLds + (t % fQC) * 8) * 2;
   const unsigned lane = t & 63, wid = t >> 6;
@@ -180,8 +182,10 @@ __device__ __forceinline__ void filter_load_q(FilterPreQ& p, const FilterAddr& a
       p.q[i] = i32x4(0);
       continue;
     }
+    // chunks past the padded row: an offset beyond the buffer (zeros)
+    const uint32_t off = c * fBK < ad.dq ? o.qg + i * ad.qs : 0x7fff0000u;
     p.q[i] = __builtin_bit_cast(
-        i32x4, __builtin_amdgcn_raw_buffer_load_b128(ad.qr, o.qg + i * ad.qs, c * fBK * 2, 0));
+        i32x4, __builtin_amdgcn_raw_buffer_load_b128(ad.qr, off, c * (fBK / 32) * ad.qb, 0));
   }
 }
 
@@ -456,18 +460,21 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
       const int nb = __builtin_amdgcn_readfirstlane((int)(rows * a.d * (int64_t)sizeof(XT)));
       ad.xr = __builtin_amdgcn_make_buffer_rsrc(
           reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
-      const uint16_t* qb = a.Qh + q0 * (int64_t)a.dq;
+      const uint16_t* qb = a.Qh + q0 * 32;
       const uint64_t qp = reinterpret_cast<uint64_t>(qb);
       const uint32_t qlo = __builtin_amdgcn_readfirstlane((uint32_t)qp);
       const uint32_t qhi = __builtin_amdgcn_readfirstlane((uint32_t)(qp >> 32));
-      const int qnb = __builtin_amdgcn_readfirstlane(fBQ * a.dq * 2);
+      const int qnb = __builtin_amdgcn_readfirstlane(
+          (int)(((int64_t)(a.dq / 32 - 1) * a.qstride + fBQ) * 64));
       ad.qr = __builtin_amdgcn_make_buffer_rsrc(
           reinterpret_cast<void*>(((uint64_t)qhi << 32) | qlo), 0, qnb, 0x00020000);
       ad.d = a.d;
       ad.xs = (uint32_t)(fThreads / X::C) * (uint32_t)a.d * (uint32_t)sizeof(XT);
-      ad.qs = (uint32_t)(fThreads / fQC) * (uint32_t)a.dq * 2u;
+      ad.qs = (uint32_t)(fThreads / fQC) * 64u;
+      ad.qb = (uint32_t)a.qstride * 64u;
+      ad.dq = a.dq;
     }
-    const FilterOff o = filter_offsets<XT>(opaque(tid), ad, a.dq);
+    const FilterOff o = filter_offsets<XT>(opaque(tid), ad);
 
     // Two register stages: chunks c + 2 and c + 3 of X are in flight while
     // chunk c is multiplied (stage j % 2 holds chunk j), the query tile one
@@ -659,9 +666,9 @@ __device__ __forceinline__ void ring_issue(unsigned char* smem, const FilterArgs
     }
     const int q = 16 * j + (lane >> 2);
     const int p = (lane & 3) ^ ((q >> 2) & 3);
-    const uint32_t voff = (uint32_t)((q * a.dq + p * 8) * 2);
+    const uint32_t voff = (uint32_t)(q * 64 + p * 16);  // blocked layout (FilterArgs::Qh)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (lds_ptr)(st + L::xbytes + j * 1024), 16, voff,
-                                             k0 * 2, 0, 0);
+                                             (int)(c * a.qstride * 64), 0, 0);
   }
 }
 
@@ -755,7 +762,8 @@ __global__ void __launch_bounds__(ring::kThreads, ring::kWaves / 4) ring_kernel(
   const int nch = (a.d + kBK - 1) / kBK;
   const int diag = a.diag;
   filter_query_table<METRIC>(a, q0, qtab, qab, tid, kThreads);
-  const __amdgpu_buffer_rsrc_t qr = make_rsrc(a.Qh + q0 * (int64_t)a.dq, (int64_t)kBQ * a.dq * 2);
+  const __amdgpu_buffer_rsrc_t qr =
+      make_rsrc(a.Qh + q0 * 32, ((int64_t)(a.dq / 32 - 1) * a.qstride + kBQ) * 64);
 
   // step sequence: (tile ti, chunk c) -> stage buffer (step % 3)
   auto tile_r0 = [&](int64_t ti) -> int64_t { return (a.tile_start + ti * a.tile_stride) * kBM; };
@@ -860,7 +868,7 @@ static int launch_ring(const FilterArgs& a, int metric, hipStream_t stream) {
   for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
     FilterArgs b = a;
     const int64_t yn = (qtiles - y0) < 65535 ? (qtiles - y0) : 65535;
-    b.Qh = a.Qh + y0 * ring::kBQ * (int64_t)a.dq;
+    b.Qh = a.Qh + y0 * ring::kBQ * 32;
     b.qinfo = a.qinfo + y0 * ring::kBQ * 4;
     b.thr = a.thr + y0 * ring::kBQ;
     b.count = a.count + y0 * ring::kBQ * kCountStride;
@@ -906,7 +914,7 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
     FilterArgs b = a;
     const int64_t yn = (qtiles - y0) < 65535 ? (qtiles - y0) : 65535;
-    b.Qh = a.Qh + y0 * fBQ * (int64_t)a.dq;
+    b.Qh = a.Qh + y0 * fBQ * 32;
     b.qinfo = a.qinfo + y0 * fBQ * 4;
     b.thr = a.thr + y0 * fBQ;
     b.count = a.count + y0 * fBQ * kCountStride;
@@ -964,9 +972,12 @@ __global__ void qprep_kernel(const float* __restrict__ Q, int64_t nq, int64_t nq
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (q >= nq_pad) return;
-  _Float16* out = reinterpret_cast<_Float16*>(Qh) + q * (int64_t)dq;
+  // blocks of 32 components, query-major inside a block (FilterArgs::Qh):
+  // a K chunk of a query tile is one contiguous run of whole cache lines
+  _Float16* out = reinterpret_cast<_Float16*>(Qh) + q * 32;
+  auto at = [&](int i) -> _Float16& { return out[(int64_t)(i >> 5) * nq_pad * 32 + (i & 31)]; };
   if (q >= nq) {
-    for (int i = lane; i < dq; i += 64) out[i] = (_Float16)0.f;
+    for (int i = lane; i < dq; i += 64) at(i) = (_Float16)0.f;
     return;
   }
   const float* qv = Q + q * (int64_t)d;
@@ -985,7 +996,7 @@ __global__ void qprep_kernel(const float* __restrict__ Q, int64_t nq, int64_t nq
   if (m > 0.f && m <= 3.4e38f) (void)frexpf(m, &ex);  // m in [2^(ex-1), 2^ex)
   const int sh = 15 - ex;
   const float scale = ldexpf(1.f, sh > 126 ? 126 : (sh < -126 ? -126 : sh));
-  for (int i = lane; i < dq; i += 64) out[i] = (_Float16)(i < d ? qv[i] * scale : 0.f);
+  for (int i = lane; i < dq; i += 64) at(i) = (_Float16)(i < d ? qv[i] * scale : 0.f);
   if (lane == 0) {
     const double u = 1.0 / 2048.0, g = 5.9604644775390625e-08;
     const double sd = sqrt((double)d);
