@@ -58,6 +58,9 @@
 #ifndef FX_FILTER_BQ
 #define FX_FILTER_BQ 256
 #endif
+#ifndef FX_FILTER_ROWS  // row types compiled: 1 f32, 2 fp16
+#define FX_FILTER_ROWS (FX_FILTER_BQ == 64 ? 3 : FX_FILTER_BK == 64 ? 2 : 1)
+#endif
 #ifndef FX_FILTER_IMPL
 #define FX_FILTER_IMPL q256
 #endif
@@ -892,17 +895,31 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   if (filter_ring()) return f16 ? launch_ring<_Float16>(a, metric, stream)
                                 : launch_ring<float>(a, metric, stream);
   const size_t smem = sizeof(FilterShared);
-  const void* fns[2][3] = {
-      {(const void*)filter_kernel<float, 0>, (const void*)filter_kernel<float, 1>,
-       (const void*)filter_kernel<float, 2>},
-      {(const void*)filter_kernel<_Float16, 0>, (const void*)filter_kernel<_Float16, 1>,
-       (const void*)filter_kernel<_Float16, 2>}};
+  // (the 256-query compilation serves f32 rows, h256 fp16 rows, q64 both)
+#if FX_FILTER_ROWS & 1
+#define FX_F32_KERNEL(m) (const void*)filter_kernel<float, m>
+#else
+#define FX_F32_KERNEL(m) nullptr
+#endif
+#if FX_FILTER_ROWS & 2
+#define FX_F16_KERNEL(m) (const void*)filter_kernel<_Float16, m>
+#else
+#define FX_F16_KERNEL(m) nullptr
+#endif
+  const void* fns[2][3] = {{FX_F32_KERNEL(0), FX_F32_KERNEL(1), FX_F32_KERNEL(2)},
+                           {FX_F16_KERNEL(0), FX_F16_KERNEL(1), FX_F16_KERNEL(2)}};
+#undef FX_F32_KERNEL
+#undef FX_F16_KERNEL
+  if (fns[f16][0] == nullptr) {
+    set_error("filter: row type not compiled into this variant");
+    return FX_EUNSUPPORTED;
+  }
   const void* fn = fns[f16][metric == FX_METRIC_COS ? 2 : metric == FX_METRIC_IP ? 1 : 0];
   static bool attr = false;
   if (!attr) {
     for (auto& row : fns)
       for (const void* f : row)
-        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (f) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
   int cus = 0;
@@ -938,6 +955,9 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
 namespace q64 {
 int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_q64.hip
 }
+namespace h256 {
+int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_h256.hip
+}
 
 // The register-staged kernel by default (measured faster for both row types:
 // 8.5 vs 10.1 ms for configs[2]; see DESIGN.md for fp16); FX_FILTER_RING=1
@@ -949,7 +969,9 @@ bool filter_ring() {
 
 // Batches of <= 64 queries take the 64-query tiles (their Qh is padded to 64)
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
-  return a.nq <= 64 ? q64::launch(a, metric, stream) : q256::launch(a, metric, stream);
+  if (a.nq <= 64) return q64::launch(a, metric, stream);
+  if (a.dtype == FX_DTYPE_F16 && !filter_ring()) return h256::launch(a, metric, stream);
+  return q256::launch(a, metric, stream);
 }
 
 // rows per tile of the kernel launch_filter picks for the dtype (the 64-query
