@@ -164,7 +164,11 @@ static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, 
   // nested samples: phase i scans every stride_i-th tile, each stride a
   // multiple of the next, so every sample contains the previous one and has
   // at least k rows under the previous threshold; ~cap/4 appends per query.
-  const int64_t r = b->cap / (4 * k);  // >= 16 for k <= 1024
+  int64_t r = b->cap / (4 * k);  // >= 16 for k <= 1024
+  if (const char* env = getenv("FX_BATCH_R")) {  // tuning knob: denser samples (never sparser)
+    const int64_t v = atoll(env);
+    if (v >= 2 && v < r) r = v;
+  }
   int64_t strides[16];
   int m = 0;
   strides[m++] = 1;
