@@ -410,6 +410,39 @@ def test_batched_filter_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq
     check_topk(fd, fr, od, orow, xh, q, metric)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+def test_batched_filter_sampling_plan_invariant(eng, monkeypatch, dtype):
+    """The nested sample phases only set thresholds: any candidate buffer size
+    and sample ratio (FX_BATCH_CAP / FX_BATCH_R, e.g. 2-5 phases) gives the
+    same rows and distances, bit for bit (every kept candidate is rescored)."""
+    n, d, nq, k = 400_000, 256, 96, 50
+    tdt = torch.float16 if dtype == "f16" else torch.float32
+    x = gpu_fill(eng, n, d, seed=31, dtype=tdt)
+    q = O.fill_normal(nq, d, seed=32)
+    if dtype == "f16":
+        q = q.astype(np.float16).astype(np.float32)
+    for v in ("FX_BATCH", "FX_BATCH_FILTER", "FX_BATCH_CAP", "FX_BATCH_R", "FX_FILTER_RING"):
+        monkeypatch.delenv(v, raising=False)
+    for metric in METRICS:
+        base_d, base_r = gpu_search(eng, x, q, metric, k)
+        for cap, r in (("", "3"), ("", "8"), ("32768", ""), (str(16 * k), "2")):
+            for var, val in (("FX_BATCH_CAP", cap), ("FX_BATCH_R", r)):
+                if val:
+                    monkeypatch.setenv(var, val)
+                else:
+                    monkeypatch.delenv(var, raising=False)
+            pd, pr = gpu_search(eng, x, q, metric, k)
+            np.testing.assert_array_equal(pr, base_r)
+            np.testing.assert_array_equal(pd.view(np.uint32), base_d.view(np.uint32))
+        monkeypatch.delenv("FX_BATCH_CAP", raising=False)
+        monkeypatch.delenv("FX_BATCH_R", raising=False)
+        monkeypatch.setenv("FX_BATCH", "0")
+        sd, sr = gpu_search(eng, x, q, metric, k)
+        monkeypatch.delenv("FX_BATCH")
+        np.testing.assert_array_equal(base_r, sr)
+        np.testing.assert_array_equal(base_d.view(np.uint32), sd.view(np.uint32))
+
+
 @pytest.mark.parametrize("metric", METRICS)
 @pytest.mark.parametrize("n,d,nq,k", [(120_000, 1536, 24, 1000), (20_003, 104, 64, 10),
                                       (50_000, 768, 256, 100)])
