@@ -5,6 +5,8 @@
 #include <stdio.h>
 
 #include <map>
+#include <set>
+#include <tuple>
 #include <vector>
 #include <mutex>
 #include <utility>
@@ -58,16 +60,47 @@ int device_cus(int* out) {
   return FX_OK;
 }
 
-int kernel_occupancy(const void* fn, int block, size_t smem, int* out) {
-  static std::map<std::pair<const void*, size_t>, int> cache;
+// The dynamic-LDS limit above 64 KB is a per-device function attribute: set
+// it once per (device, kernel), so a table sharded over several devices can
+// launch the same kernel on each of them.
+int allow_lds(const void* fn) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) {
+    set_error("hipGetDevice: %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  static std::set<std::pair<int, const void*>> done;
   std::lock_guard<std::mutex> lk(g_mu);
-  auto key = std::make_pair(fn, smem);
+  if (!done.insert(std::make_pair(dev, fn)).second) return FX_OK;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) {
+    done.erase(std::make_pair(dev, fn));
+    set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize): %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  return FX_OK;
+}
+
+int kernel_occupancy(const void* fn, int block, size_t smem, int* out) {
+  if (smem > 64 * 1024) {
+    int rc = allow_lds(fn);
+    if (rc) return rc;
+  }
+  int dev = 0;
+  hipError_t e0 = hipGetDevice(&dev);
+  if (e0 != hipSuccess) {
+    set_error("hipGetDevice: %s", hipGetErrorString(e0));
+    return FX_EHIP;
+  }
+  static std::map<std::tuple<int, const void*, size_t>, int> cache;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto key = std::make_tuple(dev, fn, smem);
   auto it = cache.find(key);
   if (it != cache.end()) {
     *out = it->second;
     return FX_OK;
   }
-  if (smem > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   int nb = 0;
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, block, smem);
   if (e != hipSuccess) {

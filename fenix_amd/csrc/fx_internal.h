@@ -134,6 +134,8 @@ void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 int check_launch(const char* what);
 int device_cus(int* out);
 int kernel_occupancy(const void* fn, int block, size_t smem, int* out);
+// raise the dynamic-LDS limit of fn to 160 KB on the current device (once per device)
+int allow_lds(const void* fn);
 
 // k above the fused path (knn_large.hip): all distances + radix sort.
 struct LargeLayout {

@@ -230,16 +230,7 @@ int launch_batch(const BatchArgs& a, int metric, hipStream_t stream) {
   const void* fn = metric == FX_METRIC_COS ? (const void*)batch_kernel<2>
                    : metric == FX_METRIC_IP ? (const void*)batch_kernel<1>
                                             : (const void*)batch_kernel<0>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)batch_kernel<2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    (void)hipFuncSetAttribute((const void*)batch_kernel<1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    (void)hipFuncSetAttribute((const void*)batch_kernel<0>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    attr = true;
-  }
+  if (int rc = allow_lds(fn)) return rc;
   int cus = 0;
   int rc = device_cus(&cus);
   if (rc) return rc;

@@ -664,7 +664,7 @@ int run_assign(const void* X, int dtype, int64_t groups, int64_t rows, int64_t d
          : metric == FX_METRIC_IP ? assign_fn<_Float16, 1>() : assign_fn<_Float16, 2>();
   }
   const size_t smem = sizeof(AssignShared);
-  (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  if (int rc2 = allow_lds((const void*)fn)) return rc2;
   int cus = 0;
   rc = device_cus(&cus);
   if (rc) return rc;

@@ -852,16 +852,7 @@ static int launch_ring(const FilterArgs& a, int metric, hipStream_t stream) {
   const void* fn = metric == FX_METRIC_COS ? (const void*)ring_kernel<XT, 2>
                    : metric == FX_METRIC_IP ? (const void*)ring_kernel<XT, 1>
                                             : (const void*)ring_kernel<XT, 0>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)ring_kernel<XT, 2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    (void)hipFuncSetAttribute((const void*)ring_kernel<XT, 1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    (void)hipFuncSetAttribute((const void*)ring_kernel<XT, 0>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    attr = true;
-  }
+  if (int rc = allow_lds(fn)) return rc;
   int cus = 0;
   int rc = device_cus(&cus);
   if (rc) return rc;
@@ -915,13 +906,7 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
     return FX_EUNSUPPORTED;
   }
   const void* fn = fns[f16][metric == FX_METRIC_COS ? 2 : metric == FX_METRIC_IP ? 1 : 0];
-  static bool attr = false;
-  if (!attr) {
-    for (auto& row : fns)
-      for (const void* f : row)
-        if (f) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    attr = true;
-  }
+  if (int rc = allow_lds(fn)) return rc;
   int cus = 0;
   int rc = device_cus(&cus);
   if (rc) return rc;

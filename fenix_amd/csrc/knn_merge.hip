@@ -184,12 +184,7 @@ int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, voi
     // the input area doubles as the rank-sort output on the final level
     const int64_t sin = G * klen > k ? G * klen : k;
     const size_t smem = sizeof(MergeShared) + (size_t)rcap * 8 + (size_t)sin * 8;
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)merge_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          160 * 1024);
-      attr_set = true;
-    }
+    if (int rc = allow_lds((const void*)merge_kernel)) return rc;
     for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
       const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
       dim3 grid((unsigned)blocks, (unsigned)qn);

@@ -749,17 +749,6 @@ static ScanKernelFn select_q8_dma_kernel(int metric, int L) {
   return pick_q8_dma<2>(L);
 }
 
-// the DMA variants may take more than the default 64 KB of dynamic LDS
-static void q8_dma_attrs() {
-  static bool done = false;
-  if (done) return;
-  for (int m = 0; m < 3; ++m)
-    for (int L : {1, 2, 3, 4})
-      (void)hipFuncSetAttribute((const void*)select_q8_dma_kernel(m, L),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  done = true;
-}
-
 ScanKernelFn select_scan_kernel(int dtype, int metric, int W, int L) {
   if (dtype == FX_DTYPE_F32) {
     if (W == 1) {
@@ -846,8 +835,10 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   rc = kernel_occupancy((const void*)p->fn, 256, smem, &occ);
   if (rc) return rc;
   if (p->fn_dma != nullptr) {  // one grid serves both variants: the smaller occupancy
-    q8_dma_attrs();
     int occ2 = 0;
+    // the DMA variants may take more than the default 64 KB of dynamic LDS
+    rc = allow_lds((const void*)p->fn_dma);
+    if (rc) return rc;
     rc = kernel_occupancy((const void*)p->fn_dma, 256, p->smem_dma, &occ2);
     if (rc) return rc;
     if (occ2 < occ) occ = occ2;
@@ -881,9 +872,12 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
 int launch_scan(const ScanPlan& p, const ScanArgs& a, int64_t nq, hipStream_t stream) {
   dim3 grid((unsigned)p.blocks, (unsigned)nq);
   if (p.fn_dma != nullptr && a.mask == nullptr && a.rows == nullptr) {
-    q8_dma_attrs();
+    if (int rc = allow_lds((const void*)p.fn_dma)) return rc;
     hipLaunchKernelGGL(p.fn_dma, grid, dim3(256), p.smem_dma, stream, a);
     return check_launch("scan_kernel (quint8 LDS-DMA)");
+  }
+  if (p.smem > 64 * 1024) {
+    if (int rc = allow_lds((const void*)p.fn)) return rc;
   }
   hipLaunchKernelGGL(p.fn, grid, dim3(256), p.smem, stream, a);
   return check_launch("scan_kernel");

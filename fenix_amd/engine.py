@@ -7,7 +7,7 @@ reference's ``io.index.call`` (src/fenix/io/index/index.py:81-170):
   table.py:12-21 -> arrow.py:6-8) and hands every chunk to a Python UDF that
   runs ``coder.distance`` on the CPU (index.py:137-162);
 * here the embedding column is staged ONCE into HBM (``stage_column``), keyed
-  by (path, size, mtime, column, device) so a rewrite by ``do_put`` restages it
+  by (path, file version, column, device) so a rewrite by ``do_put`` restages it
   (``CorpusCache``), and every search is one fused scan + merge on the GPU
   (``Engine.search`` -> ``fx_knn_search`` / ``fx_topk_merge``).
 
@@ -212,7 +212,7 @@ def stage_sharded(col: pa.ChunkedArray, devs: Sequence[torch.device]) -> List[Pi
 
 
 class CorpusCache:
-    """HBM-resident embedding columns keyed by (path, size, mtime_ns, column, devices)."""
+    """HBM-resident embedding columns keyed by (path, file version, column, devices)."""
 
     def __init__(self) -> None:
         self._lock = threading.Lock()
@@ -220,9 +220,9 @@ class CorpusCache:
 
     @staticmethod
     def _key(path: str, column: str, devs: Sequence[torch.device]) -> tuple:
-        st = os.stat(path)
-        return (os.path.abspath(path), st.st_size, st.st_mtime_ns, column,
-                tuple(str(d) for d in devs))
+        from .io.arrow import file_version
+
+        return (os.path.abspath(path), file_version(path), column, tuple(str(d) for d in devs))
 
     def get(self, path: str, table: pa.Table, column: str,
             devs: Sequence[torch.device]) -> _Entry:
@@ -232,7 +232,7 @@ class CorpusCache:
             if hit is not None:
                 return hit
             # drop stale versions of the same file/column/devices
-            for k in [k for k in self._entries if k[0] == key[0] and k[3:] == key[3:]]:
+            for k in [k for k in self._entries if k[0] == key[0] and k[2:] == key[2:]]:
                 del self._entries[k]
             entry = _Entry(key, table, stage_sharded(table.column(column), devs))
             self._entries[key] = entry
@@ -342,9 +342,14 @@ class Engine:
         ws = self._workspace(nbytes)
         od = torch.empty((nq, k), dtype=torch.float32, device=self.device)
         orow = torch.empty((nq, k), dtype=torch.int64, device=self.device)
+        # contiguous copies are held in locals until the merge is queued: a
+        # temporary freed before the launch could be handed to the next
+        # allocation (the row copy) and be read as distances
+        dist = dist.contiguous()
+        row = row.contiguous()
         _lib.check(
             _lib.load().fx_topk_merge(
-                _ptr(dist.contiguous()), _ptr(row.contiguous()), nq, parts, kin, k, _ptr(ws),
+                _ptr(dist), _ptr(row), nq, parts, kin, k, _ptr(ws),
                 ws.numel(), _ptr(od), _ptr(orow), self._stream(),
             )
         )
@@ -637,8 +642,10 @@ class DeviceComm:
         outs = [(torch.empty((n, nq, k), dtype=torch.float32, device=dv),
                  torch.empty((n, nq, k), dtype=torch.int64, device=dv)) for dv in self.devs]
         P = ctypes.c_void_p * n
-        src_d = P(*[d.contiguous().data_ptr() for d, _ in per])
-        src_r = P(*[r.contiguous().data_ptr() for _, r in per])
+        # keep the contiguous sources alive until the collective is queued
+        srcs = [(d.contiguous(), r.contiguous()) for d, r in per]
+        src_d = P(*[d.data_ptr() for d, _ in srcs])
+        src_r = P(*[r.data_ptr() for _, r in srcs])
         dst_d = P(*[d.data_ptr() for d, _ in outs])
         dst_r = P(*[r.data_ptr() for _, r in outs])
         streams = P(*[torch.cuda.current_stream(dv).cuda_stream for dv in self.devs])

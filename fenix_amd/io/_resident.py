@@ -2,7 +2,7 @@
 
 * mmap'd Arrow tables, one per file version (io.arrow.load, arrow.py:6-8, is
   re-run by the reference on every search; here it is re-run only when the
-  file's (size, mtime) changes — do_put rewrites invalidate it);
+  file's version (size, mtime, inode, rewrite count) changes — do_put rewrites invalidate it);
 * single-chunk copies of small result columns for ``take`` (index.py:166);
 * the HBM shards of embedding columns (engine.CACHE) and of index code
   columns (``__CODED_ID__``, int64 per row) used to build probe masks on the
@@ -29,8 +29,7 @@ _CODES: Dict[tuple, torch.Tensor] = {}  # (stat key, column, device) -> int64 [r
 
 
 def stat_key(path: str) -> tuple:
-    st = os.stat(path)
-    return (os.path.abspath(path), st.st_size, st.st_mtime_ns)
+    return (os.path.abspath(path),) + arrow.file_version(path)
 
 
 def load_table(path: str) -> Tuple[tuple, pa.Table]:

@@ -43,6 +43,7 @@ import torch
 from torch import Tensor
 
 from .. import _lib
+from . import arrow
 from ..engine import Engine, Shard
 
 LOCATION: str = "codings"
@@ -147,8 +148,7 @@ def load(root: str, name: str) -> Coding:
     """coder.py:68-91: read the coding, register the UDF ``name``."""
     path = _path(root, name)
     os.makedirs(os.path.dirname(path), exist_ok=True)
-    st = os.stat(path)
-    key = (st.st_size, st.st_mtime_ns)
+    key = arrow.file_version(path)
     with _lock:
         hit = _CODINGS.get(os.path.abspath(path))
         if hit is not None and hit[0] == key:
@@ -207,8 +207,10 @@ def make(root: str, name: str, source: str | Sequence[str], column: str, config:
 
     path = _path(root, name)
     os.makedirs(os.path.dirname(path), exist_ok=True)
-    with open(path, "wb") as f:
+    tmp = arrow.temp_path(path)
+    with open(tmp, "wb") as f:
         torch.save({"tensor": tensor, "column": _type_bytes(vtype), "config": dict(config)}, f)
+    arrow.replace(tmp, path)
     return load(root, name)
 
 

@@ -279,6 +279,28 @@ def test_topk_merge(eng):
         np.testing.assert_array_equal(od[i], dv[order])
 
 
+def test_topk_merge_non_contiguous_views(eng):
+    """Engine.merge of permuted [nq, parts, k] views (the RCCL gather's
+    layout, engine.DeviceComm.gather_merge): the contiguous copies must stay
+    alive until the merge is queued, or the row copy can reuse the distance
+    copy's block.  Repeated with fresh allocations so a reuse would show."""
+    rs = np.random.RandomState(5)
+    ndev, nq, k = 4, 6, 32
+    for it in range(20):
+        d = np.sort(rs.randn(ndev, nq, k).astype(np.float32), axis=2)
+        r = (rs.permutation(ndev * nq * k).reshape(ndev, nq, k) + 7).astype(np.int64)
+        td = torch.from_numpy(d).to(eng.device).permute(1, 0, 2)
+        tr = torch.from_numpy(r).to(eng.device).permute(1, 0, 2)
+        assert not td.is_contiguous() and not tr.is_contiguous()
+        od, orow = eng.merge(td, tr, k)
+        od, orow = od.cpu().numpy(), orow.cpu().numpy()
+        for i in range(nq):
+            dv, rv = d[:, i].ravel(), r[:, i].ravel()
+            order = np.lexsort((rv, dv))[:k]
+            np.testing.assert_array_equal(orow[i], rv[order])
+            np.testing.assert_array_equal(od[i], dv[order])
+
+
 def test_sharded_equals_whole(eng):
     """topk(all rows) == merge(topk(shard_0), topk(shard_1), ...) bit-exactly."""
     n, d, k = 60000, 768, 100

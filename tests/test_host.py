@@ -48,6 +48,32 @@ def test_table_roundtrip_and_listing(tmp_path):
     assert list(table.list(root)) == []
 
 
+def test_rewrite_keeps_mapped_versions_valid(tmp_path):
+    """do_put -> io.table.make rewrites a source while searches may hold its
+    mmap (the resident caches keep them across calls): the old mapping must
+    stay readable, and the version key must change even when the new file has
+    the same size and lands in the same mtime tick."""
+    from fenix_amd.io import _resident, arrow
+
+    root = str(tmp_path)
+    t1, x1 = make_source(root, "s", seed=0)
+    p = table.path(root, "s")
+    key1, mapped = _resident.load_table(p)
+    old_ns = os.stat(p).st_mtime_ns
+    t2, x2 = make_source(root, "s", seed=1)  # same shape -> same size
+    os.utime(p, ns=(old_ns, old_ns))  # force the same mtime
+    assert os.path.getsize(p) == key1[1]
+    key2, mapped2 = _resident.load_table(p)
+    assert key2 != key1
+    # the first mapping still holds the first version's bytes
+    v1 = np.stack(mapped.column("vector").to_numpy(zero_copy_only=False))
+    v2 = np.stack(mapped2.column("vector").to_numpy(zero_copy_only=False))
+    np.testing.assert_array_equal(v1, x1)
+    np.testing.assert_array_equal(v2, x2)
+    assert arrow.file_version(p) == key2[1:]
+    assert not [f for f in os.listdir(os.path.dirname(p)) if f.endswith(".tmp")]
+
+
 def test_chunk_values_honours_offsets():
     x = np.arange(40, dtype=np.float32)
     arr = pa.FixedSizeListArray.from_arrays(pa.array(x), list_size=4)
