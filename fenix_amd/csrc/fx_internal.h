@@ -28,6 +28,10 @@ struct ScanArgs {
   uint64_t* out_lists;    // topk: [nq][gridDim.x][k] composites (one list per block)
   float* out_dist;        // dist: [nq][n]
   float qscale, qshift;   // FX_DTYPE_QU8: value = qscale * (code - qshift)
+  // bit 0 clear: block b scans rows [b * rows_per_block, ...) in order; set:
+  // block steps of 16U rows dealt round-robin over the grid.  Bit 1: no
+  // software pipeline (one tile per wave in flight).  Set by launch_scan.
+  int interleave;
 };
 
 typedef void (*ScanKernelFn)(ScanArgs);
@@ -37,6 +41,7 @@ struct ScanPlan {
   int W, L, U, cap;
   size_t qbytes, smem;
   int64_t blocks, rows_per_block, nlists;
+  int interleave;  // ScanArgs::interleave for the register-tile kernels
   // quint8 rows staged by LDS-DMA (plain contiguous scans: no mask, no row
   // list); null when not applicable.  Same rows_per_block (its U divides it).
   ScanKernelFn fn_dma;

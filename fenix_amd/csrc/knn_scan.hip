@@ -46,7 +46,7 @@
 #define FX_U8 1
 #endif
 #ifndef FX_U12
-#define FX_U12 1
+#define FX_U12 2  // 768-d f32 / 1536-d f16: 4.40 vs 4.54 ms (interleaved, 10M x 768)
 #endif
 
 // Rows in flight per group for quint8 rows (separately tunable).  Converted
@@ -486,9 +486,22 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
     c.qnorm = fmaxf(sqrtf(s2), 1e-12f);
   }
 
-  const int64_t lo = (int64_t)blockIdx.x * a.rows_per_block;
-  c.hi = lo + a.rows_per_block < a.n ? lo + a.rows_per_block : a.n;
+  // A block step is 16U rows (4U per wave).  Contiguous: block b owns one
+  // range of rows_per_block.  Interleaved: block steps are dealt round-robin
+  // over the grid, so at any time the whole chip reads one window of the
+  // corpus (DRAM pages stay open across CUs: tools/hbm_sweep.hip).  Either
+  // partition gives the same result (the merge orders by (distance, row)).
   const int64_t step = 16 * U;
+  int64_t lo, gstep;
+  if (a.interleave & 1) {
+    lo = (int64_t)blockIdx.x * step;
+    c.hi = a.n;
+    gstep = (int64_t)gridDim.x * step;
+  } else {
+    lo = (int64_t)blockIdx.x * a.rows_per_block;
+    c.hi = lo + a.rows_per_block < a.n ? lo + a.rows_per_block : a.n;
+    gstep = step;
+  }
 
   uint64_t thr = kEmpty;
   int cnt = 0;
@@ -600,21 +613,21 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
       slot_n = slot_n == R - 1 ? 0 : slot_n + 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's tail loads
-  } else if (PIPE && nch == 1) {
+  } else if (PIPE && nch == 1 && !(a.interleave & 2)) {
     int64_t it = lo + (int64_t)wid * 4 * U;
     if (it < c.hi) tile_load(tA, it, 0, c);
-    for (; it < c.hi; it += 2 * step) {
-      const int64_t it1 = it + step;
+    for (; it < c.hi; it += 2 * gstep) {
+      const int64_t it1 = it + gstep;
       if (it1 < c.hi) tile_load(tB, it1, 0, c);
       tile_consume<T, W, L, U, METRIC>(tA, c, thr, cnt);
       if (it1 >= c.hi) break;
-      const int64_t it2 = it1 + step;
+      const int64_t it2 = it1 + gstep;
       if (it2 < c.hi) tile_load(tA, it2, 0, c);
       tile_consume<T, W, L, U, METRIC>(tB, c, thr, cnt);
     }
   } else {
     // rows longer than one pass (d > 16*L*W): accumulate pass by pass
-    for (int64_t it = lo + (int64_t)wid * 4 * U; it < c.hi; it += step) {
+    for (int64_t it = lo + (int64_t)wid * 4 * U; it < c.hi; it += gstep) {
       float acc[U], acc2[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) acc[u] = acc2[u] = 0.f;
@@ -664,6 +677,11 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
 }
 
 // ----------------------------------------------------- dispatch / planning --
+
+#ifndef FX_SCAN_INTERLEAVE_DEFAULT
+#define FX_SCAN_INTERLEAVE_DEFAULT 1
+#endif
+static constexpr int kInterleaveDefault = FX_SCAN_INTERLEAVE_DEFAULT;
 
 // Double-buffered tiles everywhere except 16-bit rows of >= 12 slots, where
 // the second tile (plus the f16->f32 converts) costs more occupancy than the
@@ -846,7 +864,9 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   // Two 256-thread blocks per CU already saturate HBM with the pipelined
   // tiles (sweep in profiles/), and fewer blocks mean fewer candidate lists
   // to merge.  FX_SCAN_BLOCKS_PER_CU overrides (tuning knob, microbench).
-  int cap_occ = dtype == FX_DTYPE_QU8 ? 3 : 2;
+  // Rows of >= 12 slots per lane (768-d f32, 1536-d f16 and longer): one
+  // block per CU reads as fast or faster (1536-d f16: 4.50 vs 4.66 ms).
+  int cap_occ = dtype == FX_DTYPE_QU8 ? 3 : L >= 12 ? 1 : 2;
   if (const char* env = getenv("FX_SCAN_BLOCKS_PER_CU")) cap_occ = atoi(env);
   if (cap_occ > 0 && cap_occ < occ) occ = cap_occ;
   if (occ < 1) occ = 1;
@@ -866,6 +886,16 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   p->blocks = blocks;
   p->rows_per_block = rpb > 0 ? rpb : step;
   p->nlists = blocks;  // one list per block (the epilogue folds its 4 waves)
+  // Block steps dealt round-robin over the grid for rows of >= 1 KB, each
+  // block one contiguous range below that (sweep over d and dtype:
+  // profiles/r02_scan_interleave_sweep.log).  FX_SCAN_INTERLEAVE overrides.
+  const int esize = dtype == FX_DTYPE_F32 ? 4 : dtype == FX_DTYPE_F16 ? 2 : 1;
+  p->interleave = kInterleaveDefault && d * esize >= 1024;
+  if (const char* env = getenv("FX_SCAN_INTERLEAVE")) p->interleave = atoi(env) != 0;
+  // FX_SCAN_PIPE=0: one register tile per wave in flight (tuning knob)
+  if (const char* env = getenv("FX_SCAN_PIPE")) {
+    if (atoi(env) == 0) p->interleave |= 2;
+  }
   return FX_OK;
 }
 
@@ -879,7 +909,9 @@ int launch_scan(const ScanPlan& p, const ScanArgs& a, int64_t nq, hipStream_t st
   if (p.smem > 64 * 1024) {
     if (int rc = allow_lds((const void*)p.fn)) return rc;
   }
-  hipLaunchKernelGGL(p.fn, grid, dim3(256), p.smem, stream, a);
+  ScanArgs b = a;
+  b.interleave = p.interleave;
+  hipLaunchKernelGGL(p.fn, grid, dim3(256), p.smem, stream, b);
   return check_launch("scan_kernel");
 }
 

@@ -57,6 +57,7 @@ def main():
     p.add_argument("--variants", action="store_true")
     p.add_argument("--nq", type=int, default=1)
     p.add_argument("--sweep", default="", help="d:dtype list, e.g. 128:f32,1536:f16 (occ only)")
+    p.add_argument("--interleave", default="", help="FX_SCAN_INTERLEAVE values to A/B, e.g. 0,1")
     a = p.parse_args()
     if a.sweep:
         return sweep(a)
@@ -76,10 +77,11 @@ def main():
     bound = {name: bind(path) for name, path in libs.items()}
     results = {}
 
-    def scan_variant(L, occ):
-        os.environ.pop("FX_SCAN_BLOCKS_PER_CU", None)  # max blocks = largest workspace
+    def scan_variant(L, occ, il=None):
+        os.environ["FX_SCAN_BLOCKS_PER_CU"] = "8"  # max blocks = largest workspace
         need = ctypes.c_size_t(0)
         assert L.fx_knn_workspace_bytes(n, d, 0, nq, k, ctypes.byref(need)) == 0
+        os.environ.pop("FX_SCAN_BLOCKS_PER_CU", None)
         ws = torch.empty(need.value, dtype=torch.uint8, device=eng.device)
 
         def run():
@@ -87,6 +89,12 @@ def main():
                 os.environ["FX_SCAN_BLOCKS_PER_CU"] = str(occ)
             else:
                 os.environ.pop("FX_SCAN_BLOCKS_PER_CU", None)
+            os.environ.pop("FX_SCAN_INTERLEAVE", None)
+            os.environ.pop("FX_SCAN_PIPE", None)
+            if il is not None:  # "1" / "0" interleave, "1p" / "0p": also FX_SCAN_PIPE=0
+                os.environ["FX_SCAN_INTERLEAVE"] = il[0]
+                if il.endswith("p"):
+                    os.environ["FX_SCAN_PIPE"] = "0"
             rc = L.fx_knn_scan(x.data_ptr(), 0, n, d, 0, q.data_ptr(), nq, a.metric, k, None,
                                ws.data_ptr(), ws.numel(), stream)
             assert rc == 0, L.fx_last_error()
@@ -104,9 +112,12 @@ def main():
         return run
 
     variants = {}
+    ils = a.interleave.split(",") if a.interleave else [None]
     for name, L in bound.items():
         for occ in [int(v) for v in a.occ.split(",")]:
-            variants[f"scan[{name},occ={occ or 'max'}]"] = scan_variant(L, occ)
+            for il in ils:
+                tag = "" if il is None else f",il={il}"
+                variants[f"scan[{name},occ={occ or 'max'}{tag}]"] = scan_variant(L, occ, il)
     for blocks in (1024, 2048, 4096, 8192) if nq == 1 else ():
         for nt in (0, 1):
             variants[f"stream_read[blocks={blocks},nt={nt}]"] = stream_variant(blocks, nt)
@@ -118,6 +129,8 @@ def main():
             results.setdefault(name, []).extend(ts)
         print(f"round {r} done", flush=True)
     os.environ.pop("FX_SCAN_BLOCKS_PER_CU", None)
+    os.environ.pop("FX_SCAN_INTERLEAVE", None)
+    os.environ.pop("FX_SCAN_PIPE", None)
 
     # merge (reduce) settings on the default scan
     if nq > 1:
