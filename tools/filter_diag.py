@@ -31,6 +31,7 @@ def main():
     p.add_argument("--iters", type=int, default=3)
     p.add_argument("--diags", default="0,1,2,3,4,6,7")
     p.add_argument("--dtype", default="f32", choices=["f32", "f16"])
+    p.add_argument("--envs", default="", help="';'-separated NAME=VALUE settings to A/B, e.g. FX_FILTER2=0;FX_FILTER2=1")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     eng = Engine.get(dev)
@@ -41,7 +42,12 @@ def main():
     eng.fill(q, seed=1)
     shard = Shard(x, 0)
     metric = _lib.METRICS[a.metric]
-    for dg in [int(v) for v in a.diags.split(",")]:
+    settings = [e for e in a.envs.split(";") if e] or [""]
+    runs = [(dg, e) for _ in range(2) for e in settings for dg in [int(v) for v in a.diags.split(",")]]
+    for dg, env in runs:
+        if env:
+            k, v = env.split("=", 1)
+            os.environ[k] = v
         os.environ["FX_FILTER_DIAG"] = str(dg)
         eng.scan(shard, q, metric, a.k)
         torch.cuda.synchronize()
@@ -53,7 +59,8 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
-        print(json.dumps({"diag": dg, "ms": float(np.median(ts))}), flush=True)
+        print(json.dumps({"diag": dg, "env": env, "lib": os.path.basename(_lib.LIB_PATH),
+                          "ms": float(np.median(ts))}), flush=True)
     os.environ.pop("FX_FILTER_DIAG")
 
 
