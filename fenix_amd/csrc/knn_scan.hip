@@ -520,7 +520,7 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
     unsigned char* ring = smem + a.qbytes + (size_t)4 * a.cap * 8 + 4 * 256 * 4 +
                           (size_t)__builtin_amdgcn_readfirstlane(wid) * R * kTileBytes;
     const int64_t first = lo + (int64_t)wid * 4 * U;
-    const int64_t ntile = first < c.hi ? (c.hi - first + step - 1) / step : 0;
+    const int64_t ntile = first < c.hi ? (c.hi - first + gstep - 1) / gstep : 0;
     using V = typename VecT<T, W>::type;
     typedef float f2 __attribute__((ext_vector_type(2)));
     typedef float f16v __attribute__((ext_vector_type(16)));
@@ -539,7 +539,7 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
         const int64_t jj = j;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          int64_t row = first + jj * step + u * 4 + c.grp;
+          int64_t row = first + jj * gstep + u * 4 + c.grp;
           if (row >= c.hi) row = c.hi - 1;
 #pragma unroll
           for (int cc = 0; cc < L; ++cc) {
@@ -556,7 +556,7 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
         const int64_t jj = i + R - 1;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          int64_t row = first + jj * step + u * 4 + c.grp;
+          int64_t row = first + jj * gstep + u * 4 + c.grp;
           if (row >= c.hi) row = c.hi - 1;
 #pragma unroll
           for (int cc = 0; cc < L; ++cc) {
@@ -572,7 +572,7 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
       RowTile<T, W, L, U> t;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        t.row[u] = first + i * step + u * 4 + c.grp;
+        t.row[u] = first + i * gstep + u * 4 + c.grp;
         t.valid[u] = t.row[u] < c.hi;
         t.src[u] = t.row[u];
 #pragma unroll
@@ -903,7 +903,9 @@ int launch_scan(const ScanPlan& p, const ScanArgs& a, int64_t nq, hipStream_t st
   dim3 grid((unsigned)p.blocks, (unsigned)nq);
   if (p.fn_dma != nullptr && a.mask == nullptr && a.rows == nullptr) {
     if (int rc = allow_lds((const void*)p.fn_dma)) return rc;
-    hipLaunchKernelGGL(p.fn_dma, grid, dim3(256), p.smem_dma, stream, a);
+    ScanArgs b = a;
+    b.interleave = p.interleave & 1;
+    hipLaunchKernelGGL(p.fn_dma, grid, dim3(256), p.smem_dma, stream, b);
     return check_launch("scan_kernel (quint8 LDS-DMA)");
   }
   if (p.smem > 64 * 1024) {
