@@ -94,6 +94,89 @@ __global__ void __launch_bounds__(T) k_wave(const u32x4* __restrict__ p, int64_t
   if (acc == 0x12345678u) out[blockIdx.x] = acc;
 }
 
+// the scan's pattern: 3 KB rows, 16 lanes per row (256 B per row per
+// instruction, 4 rows per wave-instruction), U rows per lane group, block
+// steps of 16U rows dealt round-robin over the grid; no arithmetic
+template <int U>
+__global__ void __launch_bounds__(256) k_rows(const u32x4* __restrict__ p, int64_t n16,
+                                              uint32_t* __restrict__ out) {
+  constexpr int S = 192;  // 16-B slots per 3 KB row
+  const int64_t rows = n16 / S;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  uint32_t acc = 0;
+  for (int64_t r0 = (int64_t)blockIdx.x * 16 * U; r0 < rows; r0 += (int64_t)gridDim.x * 16 * U) {
+    u32x4 v[U][12];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = r0 + wid * 4 * U + u * 4 + g;
+#pragma unroll
+      for (int c = 0; c < 12; ++c)
+        v[u][c] = row < rows ? __builtin_nontemporal_load(p + row * S + c * 16 + j) : u32x4(0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < 12; ++c) acc ^= v[u][c][0] ^ v[u][c][1] ^ v[u][c][2] ^ v[u][c][3];
+  }
+  if (acc == 0x12345678u) out[blockIdx.x] = acc;
+}
+
+// the same rows read as whole 1 KB wave-instructions (a wave's 4U rows are one
+// contiguous run of 12U KB; lane L of instruction i reads bytes i KB + 16 L)
+template <int U>
+__global__ void __launch_bounds__(256) k_rows_flat(const u32x4* __restrict__ p, int64_t n16,
+                                                   uint32_t* __restrict__ out) {
+  constexpr int S = 192;
+  const int64_t rows = n16 / S;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t acc = 0;
+  for (int64_t r0 = (int64_t)blockIdx.x * 16 * U; r0 < rows; r0 += (int64_t)gridDim.x * 16 * U) {
+    const int64_t w0 = (r0 + wid * 4 * U) * S;  // first 16-B slot of the wave's rows
+    const int64_t lim = rows * S;
+    u32x4 v[12 * U];
+#pragma unroll
+    for (int i = 0; i < 12 * U; ++i) {
+      const int64_t q = w0 + i * 64 + lane;
+      v[i] = q < lim ? __builtin_nontemporal_load(p + q) : u32x4(0);
+    }
+#pragma unroll
+    for (int i = 0; i < 12 * U; ++i) acc ^= v[i][0] ^ v[i][1] ^ v[i][2] ^ v[i][3];
+  }
+  if (acc == 0x12345678u) out[blockIdx.x] = acc;
+}
+
+// the batched filter's pattern: a block owns 256-row tiles (grid-stride over
+// tiles) and reads them in K chunks of KB bytes per row (all 256 rows of the
+// tile per chunk, rows 3 KB apart); 512 threads, two chunks in flight
+template <int KB>
+__global__ void __launch_bounds__(512) k_tile(const u32x4* __restrict__ p, int64_t n16,
+                                              uint32_t* __restrict__ out) {
+  constexpr int S = 192;             // 16-B slots per 3 KB row
+  constexpr int C = KB / 16;         // lanes per row per chunk
+  constexpr int P = 256 * C / 512;   // pieces per thread per chunk
+  const int64_t tiles = n16 / (S * 256);
+  const int t = threadIdx.x;
+  uint32_t acc = 0;
+  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const u32x4* base = p + tile * 256 * S;
+    for (int c = 0; c < S / C; c += 2) {
+      u32x4 v[2][P];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+          const int row = (t / C) + i * (512 / C);
+          v[h][i] = __builtin_nontemporal_load(base + row * S + (c + h) * C + t % C);
+        }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < P; ++i) acc ^= v[h][i][0] ^ v[h][i][1] ^ v[h][i][2] ^ v[h][i][3];
+    }
+  }
+  if (acc == 0x12345678u) out[blockIdx.x] = acc;
+}
+
 typedef __attribute__((address_space(3))) void* lds_ptr;
 
 // LDS-DMA: each wave streams its contiguous range through a ring of S KB
@@ -172,6 +255,21 @@ static double run(const char* name, void (*fn)(const void*, int64_t, uint32_t*, 
     hipLaunchKernelGGL((KERN<T, U, NT>), dim3(blocks), dim3(T), 0, s, (const u32x4*)p, n16, \
                        out);                                                                \
   }
+#define ROWS(NAME, KERN, U)                                                                 \
+  static void NAME(const void* p, int64_t n16, uint32_t* out, int blocks, hipStream_t s) { \
+    hipLaunchKernelGGL((KERN<U>), dim3(blocks), dim3(256), 0, s, (const u32x4*)p, n16, out);  \
+  }
+#define TILE(NAME, KB)                                                                      \
+  static void NAME(const void* p, int64_t n16, uint32_t* out, int blocks, hipStream_t s) { \
+    hipLaunchKernelGGL((k_tile<KB>), dim3(blocks), dim3(512), 0, s, (const u32x4*)p, n16, out); \
+  }
+TILE(tile_128, 128)
+TILE(tile_256, 256)
+TILE(tile_512, 512)
+ROWS(rows_1, k_rows, 1)
+ROWS(rows_2, k_rows, 2)
+ROWS(flat_1, k_rows_flat, 1)
+ROWS(flat_2, k_rows_flat, 2)
 LAUNCHER(stride_256_2_nt, k_stride, 256, 2, true)
 LAUNCHER(stride_256_4_nt, k_stride, 256, 4, true)
 LAUNCHER(stride_256_8_nt, k_stride, 256, 8, true)
@@ -202,6 +300,14 @@ int main(int argc, char** argv) {
     void (*fn)(const void*, int64_t, uint32_t*, int, hipStream_t);
     int threads;
   };
+  const bool rows_only = getenv("HBM_SWEEP_ROWS") != nullptr;
+  V rv[] = {
+      {"tile 256 rows x 128 B chunks", tile_128, 512}, {"tile 256 rows x 256 B chunks", tile_256, 512},
+      {"tile 256 rows x 512 B chunks", tile_512, 512},
+      {"rows (scan pattern) U1", rows_1, 256}, {"rows (scan pattern) U2", rows_2, 256},
+      {"rows flat 1 KB U1", flat_1, 256},      {"rows flat 1 KB U2", flat_2, 256},
+      {"stride T256 U8 nt", stride_256_8_nt, 256},
+  };
   V vs[] = {
       {"stride T256 U2 nt", stride_256_2_nt, 256},   {"stride T256 U4 nt", stride_256_4_nt, 256},
       {"stride T256 U8 nt", stride_256_8_nt, 256},   {"stride T256 U16 nt", stride_256_16_nt, 256},
@@ -212,8 +318,11 @@ int main(int argc, char** argv) {
   double best = 0;
   const char* bestn = "";
   int bestb = 0;
-  for (const V& v : vs) {
-    for (int eighths : {4, 6, 8, 10, 12, 16, 24, 32}) {
+  const V* list = rows_only ? rv : vs;
+  const int nlist = rows_only ? (int)(sizeof(rv) / sizeof(rv[0])) : (int)(sizeof(vs) / sizeof(vs[0]));
+  for (int vi = 0; vi < nlist; ++vi) {
+    const V& v = list[vi];
+    for (int eighths : {4, 8, 12, 16, 24, 32}) {
       if (v.threads * eighths > 2048 * 8) continue;
       const double t = run(v.name, v.fn, p, n16, out, cus * eighths / 8, reps);
       if (t > best) {
