@@ -673,3 +673,45 @@ def test_large_k_exceeding_rows_and_multi_shard_merge(eng):
     od, orow = O.knn(O.fill_normal(9000, d, 85), q, "inner_product", 2500)
     check_topk(dd.cpu().numpy(), rr.cpu().numpy(), od, orow, O.fill_normal(9000, d, 85), q,
                "inner_product")
+
+
+# ------------------------------------------------- scan partitions (round 2)
+
+
+@pytest.mark.parametrize("n,d,dtype", [(37, 768, torch.float32), (50_000, 768, torch.float32),
+                                       (200_003, 1536, torch.float16), (80_001, 256, torch.float32),
+                                       (70_000, 1000, torch.float32)])
+@pytest.mark.parametrize("metric", METRICS)
+def test_interleaved_scan_equals_contiguous(eng, monkeypatch, n, d, dtype, metric):
+    """Block steps dealt round-robin over the grid (FX_SCAN_INTERLEAVE=1, the
+    default for rows of >= 1 KB) and one contiguous range per block give the
+    same top-k bit for bit: unmasked, masked, row-list scans, several single
+    queries per launch (FX_BATCH=0), and distance mode."""
+    x = gpu_fill(eng, n, d, seed=71, dtype=dtype, cluster=500)
+    q = torch.from_numpy(O.fill_normal(3, d, seed=72)).to(eng.device)
+    keep = np.random.RandomState(7).rand(n) < 0.3
+    m = device_mask(keep, eng.device)
+    mid = _lib.METRICS[metric]
+    k = min(64, n)
+    monkeypatch.setenv("FX_BATCH", "0")
+    out = {}
+    for il in ("0", "1"):
+        monkeypatch.setenv("FX_SCAN_INTERLEAVE", il)
+        for pipe in ("1", "0"):
+            monkeypatch.setenv("FX_SCAN_PIPE", pipe)
+            res = [eng.search([Shard(x, 11)], q, mid, k),
+                   eng.search([Shard(x, 11)], q, mid, k, [m]),
+                   eng.search([Shard(x, 11)], q, mid, k, [m], [int(keep.sum())]),
+                   (eng.distances(Shard(x, 11), q, mid),)]
+            torch.cuda.synchronize()
+            out[(il, pipe)] = [tuple(t.cpu().numpy() for t in r) for r in res]
+    ref = out[("0", "1")]
+    for key, got in out.items():
+        for a, b in zip(ref, got):
+            for ta, tb in zip(a, b):
+                np.testing.assert_array_equal(ta.view(np.uint8), tb.view(np.uint8), err_msg=str(key))
+    # and the unmasked result is the oracle's
+    xh = O.fill_normal(n, d, 71, cluster=500,
+                       dtype=np.float32 if dtype == torch.float32 else np.float16).astype(np.float32)
+    od, orow = O.knn(xh, q.cpu().numpy(), metric, k)
+    check_topk(ref[0][0], ref[0][1] - 11, od, orow, xh, q.cpu().numpy(), metric)
