@@ -65,6 +65,10 @@ def main() -> None:
     p.add_argument("--batch", type=int, default=1000)
     p.add_argument("--reps", type=int, default=30)
     p.add_argument("--clients", type=int, default=1, help="concurrent client processes")
+    p.add_argument("--direct", action="store_true",
+                   help="write the source file in-process (io.table.make) instead of "
+                        "through Flight.make_table (large corpora)")
+    p.add_argument("--root", default="", help="server root directory (default: a temp dir)")
     p.add_argument("--no-coalesce", action="store_true",
                    help="serve every request alone (FENIX_AMD_COALESCE=0)")
     p.add_argument("--client", action="store_true")
@@ -88,7 +92,10 @@ def main() -> None:
 
     def batches():
         dev = torch.empty((a.batch, a.d), dtype=tdt, device=eng.device)
-        for s in range(0, a.n, a.batch):
+        nb = (a.n + a.batch - 1) // a.batch
+        for bi, s in enumerate(range(0, a.n, a.batch)):
+            if nb >= 20 and bi % (nb // 10) == 0:
+                print(f"ingest {bi}/{nb} batches", file=sys.stderr, flush=True)
             m = min(a.batch, a.n - s)
             eng.fill(dev[:m], seed=0, row_base=s)
             host = dev[:m].cpu().numpy()
@@ -96,14 +103,20 @@ def main() -> None:
             yield pa.record_batch([pa.array(np.arange(s, s + m, dtype=np.int64)), arr],
                                   names=["id", "vector"])
 
-    root = tempfile.mkdtemp(prefix="fenix_bench_")
+    root = tempfile.mkdtemp(prefix="fenix_bench_", dir=a.root or None)
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     server = fenix_amd.Server(root, host="127.0.0.1", port=port)
     writer = fenix_amd.Flight(host="127.0.0.1", port=port)
     t0 = time.perf_counter()
-    writer.make_table("bench/table", pa.RecordBatchReader.from_batches(schema, batches()))
+    reader = pa.RecordBatchReader.from_batches(schema, batches())
+    if a.direct:
+        from fenix_amd.io import table
+
+        table.make(root, "bench/table", reader)
+    else:
+        writer.make_table("bench/table", reader)
     t_put = time.perf_counter() - t0
     cmd = [sys.executable, os.path.abspath(__file__), "--client", "--port", str(port),
            "--d", str(a.d), "--k", str(a.k), "--metric", a.metric, "--dtype", a.dtype,
@@ -131,6 +144,7 @@ def main() -> None:
         "vectors_per_s": a.n / (med * 1e-3),
         "first_search_ms_incl_staging": res["first_ms"],
         "make_table_s": t_put,
+        "ingest": "io.table.make in the server process" if a.direct else "Flight.make_table",
         "reps": a.reps,
         "client_imported_torch": res["torch_imported"],
         "clients": a.clients,
