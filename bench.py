@@ -261,6 +261,11 @@ def main():
             "flops_per_launch": flops,
         }
     else:
+        if filt and args.dtype == "f32" and id(x) in eng._images:
+            # the phases stream the fp16 image and its row sums instead of the
+            # f32 rows: those are the bytes of the pass (the rescoring reads a
+            # few thousand f32 rows per query on top)
+            scan_bytes = n * d * 2 + n * 4 + nq * d * 4
         achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
         if filt:
             kname = ("fx::filter_kernel (fp16-MFMA bound filter, all sample phases) "
@@ -283,6 +288,7 @@ def main():
             roof["mfma_tflops"] = 2.0 * n * nq * d / (scan_ms * 1e-3) / 1e12
             roof["mfma_peak_tflops"] = MFMA_F16_PEAK_TFS
     roof["frac"] = roof["achieved"] / roof["peak"]
+    image = eng._images.get(id(x)) if filt and args.dtype == "f32" else None
 
     out = None
     if rank == 0:
@@ -315,6 +321,13 @@ def main():
                 "parallelism": f"row-shard x{world}"
                 + ((" + gloo all-gather" if gloo else " + RCCL all-gather") if world > 1 else ""),
             },
+            # the batched filter streamed the corpus's resident fp16 filter
+            # image (fx_filter_image, built in the warmup; candidates rescored
+            # from the f32 rows, results bit-identical to the f32 scan)
+            **({"filter_image": {"bytes": int(image[1].numel()) * 2 + int(image[2].numel()) * 4,
+                                 "note": "fp16 image + row sums of squares resident beside "
+                                         "the f32 corpus; FENIX_AMD_FILTER_IMAGE=0 disables"}}
+               if image is not None else {}),
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -44,6 +44,11 @@ SYMBOLS = (
     "fx_knn_search",
     "fx_knn_scan",
     "fx_knn_reduce",
+    "fx_filter_image_bytes",
+    "fx_filter_image",
+    "fx_filter_image_used",
+    "fx_knn_scan_img",
+    "fx_knn_search_img",
     "fx_knn_distances",
     "fx_topk_merge_workspace_bytes",
     "fx_topk_merge",
@@ -121,6 +126,18 @@ def load() -> ctypes.CDLL:
         L.fx_knn_reduce.argtypes = [vp, ci, i64, i64, i64, vp, i64, ci, i64, vp, vp, sz, vp, vp,
                                     vp]
         L.fx_knn_reduce.restype = ci
+        L.fx_filter_image_bytes.argtypes = [i64, i64, ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        L.fx_filter_image_bytes.restype = ci
+        L.fx_filter_image.argtypes = [vp, i64, i64, vp, vp, vp]
+        L.fx_filter_image.restype = ci
+        L.fx_filter_image_used.argtypes = [i64, i64, ci, i64, i64, ci, ctypes.POINTER(ci)]
+        L.fx_filter_image_used.restype = ci
+        L.fx_knn_scan_img.argtypes = [vp, ci, i64, i64, i64, vp, vp, vp, i64, ci, i64, vp, vp, sz,
+                                      vp]
+        L.fx_knn_scan_img.restype = ci
+        L.fx_knn_search_img.argtypes = [vp, ci, i64, i64, i64, vp, vp, vp, i64, ci, i64, vp, vp,
+                                        sz, vp, vp, vp]
+        L.fx_knn_search_img.restype = ci
         L.fx_knn_distances.argtypes = [vp, ci, i64, i64, vp, i64, ci, vp, vp, vp]
         L.fx_knn_distances.restype = ci
         L.fx_topk_merge_workspace_bytes.argtypes = [i64, i64, i64, i64, ctypes.POINTER(sz)]
@@ -192,6 +209,14 @@ def knn_workspace_bytes(n: int, d: int, dtype: int, nq: int, k: int) -> int:
     out = ctypes.c_size_t(0)
     check(load().fx_knn_workspace_bytes(n, d, dtype, nq, k, ctypes.byref(out)))
     return int(out.value)
+
+
+def filter_image_used(n: int, d: int, dtype: int, nq: int, k: int, metric: int) -> bool:
+    """True when a search of this shape runs the batched filter over f32 rows,
+    which then streams an fp16 filter image if one is given (fx_filter_image)."""
+    out = ctypes.c_int(0)
+    check(load().fx_filter_image_used(n, d, dtype, nq, k, metric, ctypes.byref(out)))
+    return bool(out.value)
 
 
 def merge_workspace_bytes(nq: int, parts: int, kin: int, k: int) -> int:

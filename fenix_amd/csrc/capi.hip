@@ -340,8 +340,11 @@ static int single_search(const void* corpus, int dtype, int64_t n, int64_t d, in
 // threshold, and only candidates whose lower bound reaches it are rescored
 // exactly (the rest are dropped unread).  fx_knn_reduce then selects the top k
 // of the exact keys and recomputes overflowing queries.
-static int filter_phases(const BatchLayout& b, const void* X, int dtype, int64_t n, int64_t d,
-                         int64_t row_base, const float* Q, int64_t nq, int metric, int64_t k,
+// With an fp16 filter image of an f32 corpus (fx_filter_image) the phases
+// stream the image (half the bytes) and the rescoring reads the f32 rows.
+static int filter_phases(const BatchLayout& b, const void* X, int dtype, const void* image,
+                         const float* rowinfo, int64_t n, int64_t d, int64_t row_base,
+                         const float* Q, int64_t nq, int metric, int64_t k,
                          const uint32_t* mask, char* w, hipStream_t st) {
   float* qnorm = reinterpret_cast<float*>(w + b.off_qnorm);
   uint64_t* thr = reinterpret_cast<uint64_t*>(w + b.off_thr);
@@ -364,8 +367,9 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, int64_t
     if (e == hipSuccess && last) e = hipMemsetAsync(cand_ub, 0xFF, (size_t)nq * b.cap * 8, st);
     if (e != hipSuccess) break;
     FilterArgs a = {};
-    a.X = X;
-    a.dtype = dtype;
+    a.X = image != nullptr ? image : X;
+    a.dtype = image != nullptr ? FX_DTYPE_F16 : dtype;
+    a.rowinfo = image != nullptr ? rowinfo : nullptr;
     a.n = n;
     a.d = (int)d;
     a.row_base = row_base;
@@ -525,9 +529,18 @@ static int search_layout(const void* corpus, int dtype, int64_t n, int64_t d, in
   return FX_OK;
 }
 
-int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
-                const float* queries, int64_t nq, int metric, int64_t k,
-                const uint32_t* mask, void* ws, size_t ws_bytes, void* stream) {
+}  // extern "C"
+
+// a filter image applies to f32 rows through the register-staged filter, with
+// rows of whole 16-B pieces (d % 8 == 0)
+static bool image_applies(const SearchLayout& s, int dtype, int64_t d) {
+  return s.batched && s.batch.filter && dtype == FX_DTYPE_F32 && d % 8 == 0 && !filter_ring();
+}
+
+static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                     const void* image, const float* rowinfo, const float* queries, int64_t nq,
+                     int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
+                     void* stream) {
   SearchLayout s;
   int rc = search_layout(corpus, dtype, n, d, nq, metric, k, ws, ws_bytes, &s);
   if (rc) return rc;
@@ -543,8 +556,13 @@ int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (s.batched) {
     if (s.batch.filter) {
-      return filter_phases(s.batch, corpus, dtype, n, d, row_base, queries, nq, metric, k, mask,
-                           reinterpret_cast<char*>(ws), st);
+      const bool img = image != nullptr && image_applies(s, dtype, d);
+      if (img && (rowinfo == nullptr || (uintptr_t)image % 16 != 0)) {
+        set_error("filter image: null row info or image not 16-byte aligned");
+        return FX_EINVAL;
+      }
+      return filter_phases(s.batch, corpus, dtype, img ? image : nullptr, rowinfo, n, d, row_base,
+                           queries, nq, metric, k, mask, reinterpret_cast<char*>(ws), st);
     }
     return batched_phases(s.batch, reinterpret_cast<const float*>(corpus), n, d, row_base,
                           queries, nq, metric, k, mask, reinterpret_cast<char*>(ws), st);
@@ -581,6 +599,78 @@ int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row
     rc = launch_scan(s.scan, a, qn, st);
     if (rc) return rc;
   }
+  return FX_OK;
+}
+
+extern "C" {
+
+int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                const float* queries, int64_t nq, int metric, int64_t k,
+                const uint32_t* mask, void* ws, size_t ws_bytes, void* stream) {
+  return scan_impl(corpus, dtype, n, d, row_base, nullptr, nullptr, queries, nq, metric, k, mask,
+                   ws, ws_bytes, stream);
+}
+
+int fx_knn_scan_img(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                    const void* image, const float* rowinfo, const float* queries, int64_t nq,
+                    int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
+                    void* stream) {
+  return scan_impl(corpus, dtype, n, d, row_base, image, rowinfo, queries, nq, metric, k, mask, ws,
+                   ws_bytes, stream);
+}
+
+int fx_filter_image_bytes(int64_t n, int64_t d, size_t* image_bytes, size_t* rowinfo_bytes) {
+  if (!image_bytes || !rowinfo_bytes) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  if (n < 0 || d < 8 || d % 8 != 0) {
+    set_error("filter image: n=%lld d=%lld (d must be a positive multiple of 8)", (long long)n,
+              (long long)d);
+    return FX_EUNSUPPORTED;
+  }
+  *image_bytes = (size_t)n * (size_t)d * 2;
+  *rowinfo_bytes = (size_t)n * 4;
+  return FX_OK;
+}
+
+int fx_filter_image(const float* corpus, int64_t n, int64_t d, void* image, float* rowinfo,
+                    void* stream) {
+  size_t ib = 0, rb = 0;
+  int rc = fx_filter_image_bytes(n, d, &ib, &rb);
+  if (rc) return rc;
+  if (n > 0 && (!corpus || !image || !rowinfo)) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  if ((uintptr_t)corpus % 16 != 0 || (uintptr_t)image % 16 != 0) {
+    set_error("filter image: corpus and image must be 16-byte aligned");
+    return FX_EINVAL;
+  }
+  if (d > 0x7fffffffll) {
+    set_error("filter image: d=%lld too large", (long long)d);
+    return FX_EUNSUPPORTED;
+  }
+  return launch_image(corpus, n, (int)d, image, rowinfo, reinterpret_cast<hipStream_t>(stream));
+}
+
+int fx_filter_image_used(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
+                         int* out) {
+  if (!out) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  *out = 0;
+  int rc = validate(n, d, dtype, nq, metric);
+  if (rc) return rc;
+  if (k < 1 || k > kLargeMaxK) {
+    set_error("k=%lld outside [1, %lld]", (long long)k, (long long)kLargeMaxK);
+    return FX_EUNSUPPORTED;
+  }
+  SearchLayout s;
+  rc = plan_search(n, d, dtype, nq, k, metric, true, &s);
+  if (rc) return rc;
+  *out = image_applies(s, dtype, d) ? 1 : 0;
   return FX_OK;
 }
 
@@ -643,6 +733,21 @@ int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
   }
   int rc = fx_knn_scan(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
                        stream);
+  if (rc) return rc;
+  return fx_knn_reduce(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
+                       out_dist, out_row, stream);
+}
+
+int fx_knn_search_img(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                      const void* image, const float* rowinfo, const float* queries, int64_t nq,
+                      int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
+                      float* out_dist, int64_t* out_row, void* stream) {
+  if (!out_dist || !out_row) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  int rc = fx_knn_scan_img(corpus, dtype, n, d, row_base, image, rowinfo, queries, nq, metric, k,
+                           mask, ws, ws_bytes, stream);
   if (rc) return rc;
   return fx_knn_reduce(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
                        out_dist, out_row, stream);

@@ -116,6 +116,8 @@ struct FilterArgs {
   uint64_t* cand;         // [nq][cap] ub composites (cand_ub null) or lb composites
   uint64_t* cand_ub;      // [nq][cap] ub composites, or null (sampling phases)
   int cap;
+  const float* rowinfo;   // [n] row sums of squares of the f32 rows when X is their fp16
+                          // filter image (dtype F16), NaN = forced; null otherwise
   int diag;               // FX_FILTER_DIAG (profiling only): 1 no appends, 2 no epilogue,
                           // 4 no MFMA, 8 no query loads, 16 no LDS stores
 };
@@ -126,6 +128,8 @@ bool filter_ring();
 int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
                  uint16_t* Qh, float* qinfo, hipStream_t stream);
 int filter_tile_rows(int dtype);
+// fp16 filter image + row sums of squares of an f32 corpus (knn_filter.hip)
+int launch_image(const float* X, int64_t n, int d, void* img, float* rowinfo, hipStream_t stream);
 int filter_query_pad(int64_t nq);
 int filter_dq(int d);
 int batch_tile_rows();

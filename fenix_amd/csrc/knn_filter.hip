@@ -210,7 +210,9 @@ __device__ __forceinline__ void filter_load(FilterPre<XT>& p, const FilterAddr& 
 // directly, and the max |x| for the fp16-overflow test), fp16 rows as they
 // are (sums of squares of the exact f32 values; an fp16 row cannot overflow,
 // an infinity or NaN shows in the sum), the query pieces as they are.
-template <typename XT, int BUF>
+// IMG: the rows are the fp16 filter image of an f32 corpus (fx_filter_image);
+// their row values come from FilterArgs::rowinfo instead.
+template <typename XT, int BUF, bool IMG>
 __device__ __forceinline__ void filter_store(const FilterPre<XT>& p, const FilterPreQ& pq,
                                              unsigned char* smem, const FilterOff& o,
                                              f32x2 (&sq)[XPiece<XT>::P],
@@ -229,11 +231,13 @@ __device__ __forceinline__ void filter_store(const FilterPre<XT>& p, const Filte
                     fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
     } else {
       lds_at<i32x4>(smem, at) = p.x[i];
-      const f16x8 h = __builtin_bit_cast(f16x8, p.x[i]);
+      if constexpr (!IMG) {
+        const f16x8 h = __builtin_bit_cast(f16x8, p.x[i]);
 #pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        const f32x2 v = {(float)h[e], (float)h[e + 1]};
-        sq[i] = __builtin_elementwise_fma(v, v, sq[i]);
+        for (int e = 0; e < 8; e += 2) {
+          const f32x2 v = {(float)h[e], (float)h[e + 1]};
+          sq[i] = __builtin_elementwise_fma(v, v, sq[i]);
+        }
       }
     }
   }
@@ -416,8 +420,9 @@ __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], cons
     }
 }
 
-template <typename XT, int METRIC>
+template <typename XT, int METRIC, bool IMG>
 __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_kernel(FilterArgs a) {
+  static_assert(!IMG || sizeof(XT) == 2, "the filter image is fp16");
   using X = XPiece<XT>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   FilterShared* sh = reinterpret_cast<FilterShared*>(smem);
@@ -489,7 +494,7 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     filter_load_q(pq, ad, o, 0, diag);
     filter_load(pf[0], ad, o, 0);
     filter_load(pf[1], ad, o, 1);
-    filter_store<XT, 0>(pf[0], pq, smem, o, sq, mx);
+    filter_store<XT, 0, IMG>(pf[0], pq, smem, o, sq, mx);
     // Q one chunk ahead, issued before the X load of the same step: vmcnt
     // retires loads in issue order, so waiting for Q(c + 1) at step c waits
     // for X(c + 1) (needed there anyway) and nothing issued later.
@@ -504,7 +509,7 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     auto step = [&](int c, FilterPre<XT>& p, auto buf) {
       constexpr int B = decltype(buf)::value;
       if (!(diag & 4)) filter_compute<B>(acc, smem, o);
-      if (!(diag & 16)) filter_store<XT, B ^ 1>(p, pq, smem, o, sq, mx);
+      if (!(diag & 16)) filter_store<XT, B ^ 1, IMG>(p, pq, smem, o, sq, mx);
       filter_load_q(pq, ad, o, c + 2, diag);
       filter_load(p, ad, o, c + 3);
       __syncthreads();
@@ -520,23 +525,25 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     // c + 1, if any, in stage 1); one-sided branches only, so the
     // accumulators need no copies at a join
     const bool two = c + 1 < nch;
-    if (two && !(diag & 16)) filter_store<XT, 1>(pf[1], pq, smem, o, sq, mx);
+    if (two && !(diag & 16)) filter_store<XT, 1, IMG>(pf[1], pq, smem, o, sq, mx);
     __syncthreads();
     if (!(diag & 4)) filter_compute<0>(acc, smem, o);
     if (two && !(diag & 4)) filter_compute<1>(acc, smem, o);
 
-    // per-row value rv from |x|^2 (the fRowLanes lanes of a row hold partials):
-    // cosine max(|x|, 1e-12), IP |x|, L2 |x|^2; NaN = forced through (fp16
-    // overflow: a component >= 65520; non-finite); -1 = skipped (past n or
-    // masked out)
+    // per-row value rv from |x|^2 (the fRowLanes lanes of a row hold partials;
+    // IMG: the f32 row's, precomputed): cosine max(|x|, 1e-12), IP |x|, L2
+    // |x|^2; NaN = forced through (fp16 overflow: a component >= 65520;
+    // non-finite); -1 = skipped (past n or masked out)
     float sqs[X::P];
 #pragma unroll
     for (int i = 0; i < X::P; ++i) {
       sqs[i] = sq[i][0] + sq[i][1];
+      if constexpr (!IMG) {
 #pragma unroll
-      for (int m = 1; m < X::C; m <<= 1) {
-        sqs[i] += __shfl_xor(sqs[i], m);
-        mx[i] = fmaxf(mx[i], __shfl_xor(mx[i], m));
+        for (int m = 1; m < X::C; m <<= 1) {
+          sqs[i] += __shfl_xor(sqs[i], m);
+          mx[i] = fmaxf(mx[i], __shfl_xor(mx[i], m));
+        }
       }
     }
 #pragma unroll
@@ -545,6 +552,7 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
         const int lr = (i * fThreads + tid) / X::C;
         const int64_t row = r0 + lr;
         bool ok = row < a.n;
+        if constexpr (IMG) sqs[i] = ok ? a.rowinfo[row] : 0.f;
         if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
         float rv;
         if constexpr (METRIC == 0) {
@@ -883,29 +891,38 @@ static int launch_ring(const FilterArgs& a, int metric, hipStream_t stream) {
 int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.num_tiles <= 0) return FX_OK;
   const bool f16 = a.dtype == FX_DTYPE_F16;
+  if (filter_ring() && a.rowinfo != nullptr) {
+    set_error("filter: the LDS-DMA ring does not read a filter image");
+    return FX_EUNSUPPORTED;
+  }
   if (filter_ring()) return f16 ? launch_ring<_Float16>(a, metric, stream)
                                 : launch_ring<float>(a, metric, stream);
   const size_t smem = sizeof(FilterShared);
   // (the 256-query compilation serves f32 rows, h256 fp16 rows, q64 both)
 #if FX_FILTER_ROWS & 1
-#define FX_F32_KERNEL(m) (const void*)filter_kernel<float, m>
+#define FX_F32_KERNEL(m) (const void*)filter_kernel<float, m, false>
 #else
 #define FX_F32_KERNEL(m) nullptr
 #endif
 #if FX_FILTER_ROWS & 2
-#define FX_F16_KERNEL(m) (const void*)filter_kernel<_Float16, m>
+#define FX_F16_KERNEL(m) (const void*)filter_kernel<_Float16, m, false>
+#define FX_IMG_KERNEL(m) (const void*)filter_kernel<_Float16, m, true>
 #else
 #define FX_F16_KERNEL(m) nullptr
+#define FX_IMG_KERNEL(m) nullptr
 #endif
-  const void* fns[2][3] = {{FX_F32_KERNEL(0), FX_F32_KERNEL(1), FX_F32_KERNEL(2)},
-                           {FX_F16_KERNEL(0), FX_F16_KERNEL(1), FX_F16_KERNEL(2)}};
+  const void* fns[3][3] = {{FX_F32_KERNEL(0), FX_F32_KERNEL(1), FX_F32_KERNEL(2)},
+                           {FX_F16_KERNEL(0), FX_F16_KERNEL(1), FX_F16_KERNEL(2)},
+                           {FX_IMG_KERNEL(0), FX_IMG_KERNEL(1), FX_IMG_KERNEL(2)}};
 #undef FX_F32_KERNEL
 #undef FX_F16_KERNEL
-  if (fns[f16][0] == nullptr) {
+#undef FX_IMG_KERNEL
+  const int rt = a.rowinfo != nullptr ? 2 : f16 ? 1 : 0;
+  if ((a.rowinfo != nullptr && !f16) || fns[rt][0] == nullptr) {
     set_error("filter: row type not compiled into this variant");
     return FX_EUNSUPPORTED;
   }
-  const void* fn = fns[f16][metric == FX_METRIC_COS ? 2 : metric == FX_METRIC_IP ? 1 : 0];
+  const void* fn = fns[rt][metric == FX_METRIC_COS ? 2 : metric == FX_METRIC_IP ? 1 : 0];
   if (int rc = allow_lds(fn)) return rc;
   int cus = 0;
   int rc = device_cus(&cus);
@@ -1038,6 +1055,56 @@ int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int 
   hipLaunchKernelGGL(qprep_kernel, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, stream, Q,
                      nq, nq_pad, d, dq, metric, Qh, qinfo);
   return check_launch("qprep_kernel");
+}
+
+// The fp16 filter image of an f32 corpus (fx_filter_image): every component
+// converted exactly as the f32 filter converts it in registers (round to
+// nearest even), plus per row the f32 sum of squares of the original
+// components, NaN when the row must be forced through (non-finite, or a
+// component >= 65520 that becomes an fp16 infinity).  The filter then streams
+// 2 bytes per component instead of 4 and skips its in-loop conversion and row
+// sums; candidates are still rescored from the f32 rows, so results do not
+// change.  One wave per row, grid-stride.
+typedef float img_f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 img_f16x4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) image_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                    _Float16* __restrict__ img,
+                                                    float* __restrict__ rowinfo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += nw) {
+    const img_f32x4* xr = reinterpret_cast<const img_f32x4*>(X + r * d);
+    img_f16x4* ir = reinterpret_cast<img_f16x4*>(img + r * d);
+    float s = 0.f, m = 0.f;
+    for (int i = lane; i < d / 4; i += 64) {
+      const img_f32x4 v = __builtin_nontemporal_load(xr + i);
+      ir[i] = __builtin_convertvector(v, img_f16x4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s = fmaf(v[e], v[e], s);
+        m = fmaxf(m, fabsf(v[e]));
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      s += __shfl_xor(s, o);
+      m = fmaxf(m, __shfl_xor(m, o));
+    }
+    if (lane == 0) rowinfo[r] = (s <= 3.4e38f && m < 65520.f) ? s : __builtin_nanf("");
+  }
+}
+
+int launch_image(const float* X, int64_t n, int d, void* img, float* rowinfo,
+                 hipStream_t stream) {
+  if (n <= 0) return FX_OK;
+  int cus = 0;
+  int rc = device_cus(&cus);
+  if (rc) return rc;
+  int64_t blocks = (n + 3) / 4;
+  if (blocks > (int64_t)cus * 32) blocks = (int64_t)cus * 32;
+  hipLaunchKernelGGL(image_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, n, d,
+                     reinterpret_cast<_Float16*>(img), rowinfo);
+  return check_launch("image_kernel");
 }
 
 #endif  // FX_FILTER_VARIANT

@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -256,6 +257,9 @@ class Engine:
         self.device = device
         self.lock = threading.Lock()
         self._ws: Optional[torch.Tensor] = None
+        # fp16 filter images of f32 corpora, by id of the corpus tensor:
+        # (signature, image, rowinfo); dropped when the tensor is collected
+        self._images: Dict[int, tuple] = {}
 
     @classmethod
     def get(cls, device: Optional[torch.device] = None) -> "Engine":
@@ -280,6 +284,41 @@ class Engine:
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
+    def filter_image(self, shard: Shard, nq: int, k: int,
+                     metric: int) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+        """The fp16 filter image (+ row sums of squares) of an f32 shard for a
+        search that runs the batched filter (fx_filter_image_used), built on
+        first use and kept while the corpus tensor lives and is unmodified
+        (its data pointer, shape and torch version counter); (None, None) when
+        the search does not read one, when ``FENIX_AMD_FILTER_IMAGE=0``, or
+        when free HBM cannot hold it.  Results never depend on it: the filter
+        only selects candidates, which are rescored from the f32 rows."""
+        if (shard.dtype_id != _lib.DTYPE_F32 or nq < 2
+                or os.environ.get("FENIX_AMD_FILTER_IMAGE", "1") == "0"
+                or not _lib.filter_image_used(shard.n, shard.d, shard.dtype_id, nq, k, metric)):
+            return None, None
+        t = shard.data
+        if not t.is_contiguous():
+            return None, None
+        key = id(t)
+        sig = (t.data_ptr(), tuple(t.shape), t._version)
+        hit = self._images.get(key)
+        if hit is not None and hit[0] == sig:
+            return hit[1], hit[2]
+        self._images.pop(key, None)  # a stale image: free it before building the new one
+        n, d = shard.n, shard.d
+        need = n * d * 2 + n * 4
+        free, _ = torch.cuda.mem_get_info(self.device)
+        if need + (1 << 30) > free:
+            return None, None
+        img = torch.empty((n, d), dtype=torch.float16, device=self.device)
+        info = torch.empty((n,), dtype=torch.float32, device=self.device)
+        _lib.check(_lib.load().fx_filter_image(_ptr(t), n, d, _ptr(img), _ptr(info),
+                                               self._stream()))
+        self._images[key] = (sig, img, info)
+        weakref.finalize(t, self._images.pop, key, None)
+        return img, info
+
     def search_shard(self, shard: Shard, queries: torch.Tensor, metric: int, k: int,
                      mask: Optional[torch.Tensor], out_dist: torch.Tensor,
                      out_row: torch.Tensor) -> None:
@@ -290,11 +329,12 @@ class Engine:
             return
         nbytes = _lib.knn_workspace_bytes(shard.n, shard.d, shard.dtype_id, nq, k)
         ws = self._workspace(nbytes)
+        img, info = self.filter_image(shard, nq, k, metric)
         _lib.check(
-            _lib.load().fx_knn_search(
+            _lib.load().fx_knn_search_img(
                 _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base,
-                _ptr(queries), nq, metric, k, _ptr(mask), _ptr(ws), ws.numel(),
-                _ptr(out_dist), _ptr(out_row), self._stream(),
+                _ptr(img), _ptr(info), _ptr(queries), nq, metric, k, _ptr(mask), _ptr(ws),
+                ws.numel(), _ptr(out_dist), _ptr(out_row), self._stream(),
             )
         )
 
@@ -315,10 +355,12 @@ class Engine:
         nq = queries.shape[0]
         nbytes = _lib.knn_workspace_bytes(shard.n, shard.d, shard.dtype_id, nq, k)
         ws = self._workspace(nbytes)
+        img, info = self.filter_image(shard, nq, k, metric)
         _lib.check(
-            _lib.load().fx_knn_scan(
+            _lib.load().fx_knn_scan_img(
                 _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base,
-                _ptr(queries), nq, metric, k, _ptr(mask), _ptr(ws), ws.numel(), self._stream(),
+                _ptr(img), _ptr(info), _ptr(queries), nq, metric, k, _ptr(mask), _ptr(ws),
+                ws.numel(), self._stream(),
             )
         )
         return ws
@@ -523,6 +565,9 @@ class Engine:
         _lib.check(
             _lib.load().fx_fill_normal(_ptr(out), dt, n, d, seed, row_base, cluster, self._stream())
         )
+        # written behind torch's back: bump the version counter that cached
+        # derived data (filter images) is keyed on
+        torch.autograd.graph.increment_version(out)
 
 
 def bitmap(mask: np.ndarray) -> np.ndarray:

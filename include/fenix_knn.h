@@ -121,6 +121,37 @@ int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
                   int64_t* out_row, void* stream);
 
 /*
+ * fp16 filter image of a float32 corpus, a resident companion of the corpus
+ * (HBM is 288 GB per GPU; the image is half the corpus).  fx_filter_image
+ * writes image [n][d] fp16 (each component rounded to nearest, as the batched
+ * filter converts it) and rowinfo [n] float32 (the row's sum of squares; NaN
+ * marks a row the filter must pass: non-finite, or a component that overflows
+ * fp16).  d must be a multiple of 8; corpus and image 16-B aligned.  The
+ * image must be rebuilt whenever the corpus changes.
+ * fx_knn_scan_img / fx_knn_search_img = fx_knn_scan / fx_knn_search (same
+ * workspace, same results bit for bit; fx_knn_reduce completes either) whose
+ * batched filter phases stream the image instead of the float32 rows; the
+ * candidates are still rescored from the float32 rows.  fx_filter_image_used
+ * says whether a search of that shape reads the image at all (batched
+ * float32 queries through the filter), so a caller builds it only then.
+ * Replaces nothing in the reference: the per-chunk UDF reads the float32
+ * column every time (src/fenix/io/index/index.py:137-162).
+ */
+int fx_filter_image_bytes(int64_t n, int64_t d, size_t* image_bytes, size_t* rowinfo_bytes);
+int fx_filter_image(const float* corpus, int64_t n, int64_t d, void* image, float* rowinfo,
+                    void* stream);
+int fx_filter_image_used(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
+                         int* out);
+int fx_knn_scan_img(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                    const void* image, const float* rowinfo, const float* queries, int64_t nq,
+                    int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
+                    void* stream);
+int fx_knn_search_img(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                      const void* image, const float* rowinfo, const float* queries, int64_t nq,
+                      int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
+                      float* out_dist, int64_t* out_row, void* stream);
+
+/*
  * fx_knn_search over a list of corpus rows instead of all of them: rows
  * [nrows] int32 local row numbers (< n, device), e.g. the rows kept by a
  * filter or a probe set (fx_mask_compact).  The scan reads only the listed

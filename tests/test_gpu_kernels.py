@@ -549,6 +549,110 @@ def test_batched_f16_extreme_rows_and_queries(eng, monkeypatch, metric, ring):
     np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
 
 
+# ------------------------------------------------------- fp16 filter image
+
+
+def _extreme_rows(n, d, seed):
+    xh = O.fill_normal(n, d, seed)
+    rs = np.random.RandomState(seed)
+    sel = rs.choice(n, 48, replace=False)
+    xh[sel[:8]] *= 1e5                      # beyond fp16 range: forced through
+    xh[sel[8:16]] *= 1e-7                   # fp16 subnormal range
+    xh[sel[16:20], 3] = np.inf
+    xh[sel[20:24], 7] = np.nan
+    xh[sel[24:28]] = 0.0
+    xh[sel[28:36]] *= 3e4                   # just below fp16 max
+    xh[sel[36:40], 5] = 65519.0             # rounds to 65504: finite
+    xh[sel[40:44], 5] = 65520.0             # rounds to infinity: forced
+    xh[sel[44:48], 1] = -np.inf
+    return xh
+
+
+def test_filter_image_contents(eng):
+    """fx_filter_image: each component rounded to nearest-even fp16 (torch's
+    own conversion, bit for bit, infinities included), rowinfo = the row's sum
+    of squares (float64 reference, 1e-5), NaN exactly for the rows the filter
+    must force through (non-finite, or a component >= 65520)."""
+    n, d = 5_003, 136
+    xh = _extreme_rows(n, d, 41)
+    x = torch.from_numpy(xh).to(eng.device)
+    img = torch.empty((n, d), dtype=torch.float16, device=eng.device)
+    info = torch.empty((n,), dtype=torch.float32, device=eng.device)
+    _lib.check(_lib.load().fx_filter_image(x.data_ptr(), n, d, img.data_ptr(), info.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(img.cpu().numpy().view(np.uint16),
+                                  x.half().cpu().numpy().view(np.uint16))
+    got = info.cpu().numpy()
+    with np.errstate(over="ignore", invalid="ignore"):
+        ss = np.sum(xh.astype(np.float64) ** 2, axis=1)
+        forced = ~np.isfinite(ss) | (ss > 3.4e38) | (np.nanmax(np.abs(xh), axis=1) >= 65520.0)
+    forced |= np.isnan(xh).any(axis=1)
+    np.testing.assert_array_equal(np.isnan(got), forced)
+    np.testing.assert_allclose(got[~forced], ss[~forced], rtol=1e-5, atol=1e-30)
+    # argument checks: d not a multiple of 8, misaligned image
+    rc = _lib.load().fx_filter_image(x.data_ptr(), n, 100, img.data_ptr(), info.data_ptr(), None)
+    assert rc != 0
+    rc = _lib.load().fx_filter_image(x.data_ptr(), n, d, img.data_ptr() + 2, info.data_ptr(), None)
+    assert rc != 0
+
+
+@pytest.mark.parametrize("metric", METRICS)
+@pytest.mark.parametrize("n,d,nq,k", [(100_000, 768, 40, 100), (60_000, 256, 256, 64),
+                                      (30_000, 64, 2, 300), (20_000, 136, 70, 25)])
+def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k):
+    """Batched f32 searches through the fp16 filter image (the default) equal
+    the same searches without it (FENIX_AMD_FILTER_IMAGE=0) and the
+    single-query scan, bit for bit, over rows the image cannot represent
+    (beyond fp16 range, infinities, NaN, subnormal, zero)."""
+    xh = _extreme_rows(n, d, 43)
+    x = torch.from_numpy(xh).to(eng.device)
+    q = O.fill_normal(nq, d, seed=44)
+    q[0] *= 2.0 ** 50
+    q[min(1, nq - 1)] = xh[7] if nq > 1 else q[0]
+    for v in ("FX_BATCH", "FX_BATCH_FILTER", "FX_FILTER_RING", "FENIX_AMD_FILTER_IMAGE"):
+        monkeypatch.delenv(v, raising=False)
+    assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, nq, k, _lib.METRICS[metric])
+    eng._images.clear()
+    id_, ir = gpu_search(eng, x, q, metric, k)
+    assert id(x) in eng._images  # the image path ran
+    monkeypatch.setenv("FENIX_AMD_FILTER_IMAGE", "0")
+    nd, nr = gpu_search(eng, x, q, metric, k)
+    monkeypatch.setenv("FX_BATCH", "0")
+    sd, sr = gpu_search(eng, x, q, metric, k)
+    for dd, rr in ((id_, ir), (nd, nr)):
+        np.testing.assert_array_equal(rr, sr)
+        np.testing.assert_array_equal(dd.view(np.uint32), sd.view(np.uint32))
+
+
+def test_filter_image_follows_corpus_changes(eng, monkeypatch):
+    """The cached image is keyed on the corpus tensor's version: an in-place
+    torch update and a rewrite through Engine.fill both rebuild it, so the
+    batched results keep equalling the scan's."""
+    n, d, nq, k = 50_000, 128, 32, 20
+    for v in ("FX_BATCH", "FX_BATCH_FILTER", "FX_FILTER_RING", "FENIX_AMD_FILTER_IMAGE"):
+        monkeypatch.delenv(v, raising=False)
+    x = gpu_fill(eng, n, d, seed=51)
+    q = O.fill_normal(nq, d, seed=52)
+    gpu_search(eng, x, q, "l2", k)
+    first = eng._images[id(x)][1]
+    for change in (lambda: x.mul_(-0.5), lambda: eng.fill(x, 53)):
+        change()
+        monkeypatch.delenv("FX_BATCH", raising=False)
+        bd, br = gpu_search(eng, x, q, "l2", k)
+        assert eng._images[id(x)][1] is not first
+        first = eng._images[id(x)][1]
+        monkeypatch.setenv("FX_BATCH", "0")
+        sd, sr = gpu_search(eng, x, q, "l2", k)
+        np.testing.assert_array_equal(br, sr)
+        np.testing.assert_array_equal(bd.view(np.uint32), sd.view(np.uint32))
+    key = id(x)
+    del x
+    import gc
+    gc.collect()
+    assert key not in eng._images
+
+
 # ---------------------------------------------------------------- row lists
 
 
