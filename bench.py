@@ -245,8 +245,12 @@ def main():
     # (fx_knn_scan takes the batched path from 2 queries, 8 without the filter:
     # f32 with d % 4 == 0, f16 with d % 8 == 0 through the filter only)
     filt_on = os.environ.get("FX_BATCH_FILTER", "1") != "0"
-    batched = nq >= (2 if filt_on else 8) and ((args.dtype == "f32" and d % 4 == 0)
-                                            or (args.dtype == "f16" and d % 8 == 0 and filt_on))
+    min_q = 2 if filt_on else 8  # capi.hip use_batched (FX_BATCH_MIN=1: single queries too)
+    if os.environ.get("FX_BATCH_MIN"):
+        min_q = int(os.environ["FX_BATCH_MIN"]) if int(os.environ["FX_BATCH_MIN"]) >= 1 else 2
+    batched = (os.environ.get("FX_BATCH", "1") != "0" and nq >= min_q
+               and ((args.dtype == "f32" and d % 4 == 0)
+                    or (args.dtype == "f16" and d % 8 == 0 and filt_on)))
     filt = batched and filt_on
     if batched and not filt:
         flops = 2.0 * n * nq * d

@@ -73,7 +73,17 @@ int allow_lds(const void* fn) {
   static std::set<std::pair<int, const void*>> done;
   std::lock_guard<std::mutex> lk(g_mu);
   if (!done.insert(std::make_pair(dev, fn)).second) return FX_OK;
-  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  // the dynamic share of the 160 KB: whatever the kernel's static __shared__
+  // variables leave
+  hipFuncAttributes at = {};
+  e = hipFuncGetAttributes(&at, fn);
+  if (e != hipSuccess) {
+    done.erase(std::make_pair(dev, fn));
+    set_error("hipFuncGetAttributes: %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          160 * 1024 - (int)at.sharedSizeBytes);
   if (e != hipSuccess) {
     done.erase(std::make_pair(dev, fn));
     set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize): %s", hipGetErrorString(e));
@@ -176,7 +186,9 @@ static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool align
   }
   int64_t min_q = kBatchMinQ;
   if (!use_filter()) min_q = 8;  // the fp32-MFMA kernel breaks even with scans at ~8 queries
-  if (const char* env = getenv("FX_BATCH_MIN")) min_q = atoll(env) > 1 ? atoll(env) : 2;
+  // FX_BATCH_MIN=1 also sends single queries through the filter (with a
+  // filter image that halves their bytes; the default keeps the exact scan)
+  if (const char* env = getenv("FX_BATCH_MIN")) min_q = atoll(env) >= 1 ? atoll(env) : 2;
   if (nq < min_q || !aligned) return false;
   // the rescoring repeats the scan's 16-B slot order: f32 rows need d % 4 == 0,
   // f16 rows d % 8 == 0 (and the fp16 filter: the fp32-MFMA kernel reads f32 only)

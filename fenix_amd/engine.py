@@ -293,7 +293,7 @@ class Engine:
         the search does not read one, when ``FENIX_AMD_FILTER_IMAGE=0``, or
         when free HBM cannot hold it.  Results never depend on it: the filter
         only selects candidates, which are rescored from the f32 rows."""
-        if (shard.dtype_id != _lib.DTYPE_F32 or nq < 2
+        if (shard.dtype_id != _lib.DTYPE_F32
                 or os.environ.get("FENIX_AMD_FILTER_IMAGE", "1") == "0"
                 or not _lib.filter_image_used(shard.n, shard.d, shard.dtype_id, nq, k, metric)):
             return None, None

@@ -625,6 +625,29 @@ def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k):
         np.testing.assert_array_equal(dd.view(np.uint32), sd.view(np.uint32))
 
 
+@pytest.mark.parametrize("metric", METRICS)
+def test_single_query_through_filter_image(eng, monkeypatch, metric):
+    """FX_BATCH_MIN=1: single queries take the batched filter over the image
+    (64-query tiles, one live query) and still equal the scan bit for bit."""
+    n, d, k = 80_000, 256, 100
+    xh = _extreme_rows(n, d, 45)
+    x = torch.from_numpy(xh).to(eng.device)
+    for v in ("FX_BATCH", "FX_BATCH_FILTER", "FX_FILTER_RING", "FENIX_AMD_FILTER_IMAGE"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("FX_BATCH_MIN", "1")
+    assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, 1, k, _lib.METRICS[metric])
+    for seed in (46, 47):
+        q = O.fill_normal(1, d, seed=seed)
+        fd, fr = gpu_search(eng, x, q, metric, k)
+        monkeypatch.setenv("FX_BATCH", "0")
+        sd, sr = gpu_search(eng, x, q, metric, k)
+        monkeypatch.delenv("FX_BATCH")
+        np.testing.assert_array_equal(fr, sr)
+        np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
+    monkeypatch.delenv("FX_BATCH_MIN")
+    assert not _lib.filter_image_used(n, d, _lib.DTYPE_F32, 1, k, _lib.METRICS[metric])
+
+
 def test_filter_image_follows_corpus_changes(eng, monkeypatch):
     """The cached image is keyed on the corpus tensor's version: an in-place
     torch update and a rewrite through Engine.fill both rebuild it, so the
