@@ -115,10 +115,17 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+// Per-tile row flags for the epilogue, by tile parity: [forced | skipped][8]
+// 32-bit masks, one per (64-row group, lane half) in the bit order of the
+// lane's 32 accumulator rows (filter_row_bit)
+constexpr int kRowFlagWords = 2 * 8;
+static_assert(fBM <= 256, "row flag words: (64-row group, lane half) <= 8");
 struct FilterShared {
   _Float16 xs[2][fBM * fLds];
   _Float16 qs[2][fBQ * fLds];
   float rinfo[fBM];  // per-row bound factor (see the epilogue)
+  float rterm[fBM];  // cosine: 1 / rinfo (the appends' bound term)
+  uint32_t rflags[2][kRowFlagWords];
   f32x4 qtab[fBQ];   // per query: the bound's constants {c1, c0, A, B}
   float2 qab[fBQ];   // per query: pass iff product >= a * row value + b
 };
@@ -324,13 +331,38 @@ __device__ __forceinline__ void filter_query_table(const FilterArgs& a, int64_t 
   }
 }
 
-// Epilogue of one tile: pass test per (row, query) — one fma and a compare
-// (see filter_query_table; extra passes only cost a rescored candidate); the
-// lane's passes over its 32 rows are collected in a bit mask per query
-// column, one atomic per (lane, column) reserves their slots.  Forced rows
-// (rinfo NaN) always pass, skipped rows (rinfo < 0) never.
+// Where local row lr of a 256-row tile sits in the epilogue's masks: the
+// word of its (64-row group, lane half) and its bit there, j with
+// lr = 64 rg + 4 h + roff(j) (filter_epilogue).
+__device__ __forceinline__ void filter_row_bit(int lr, int& word, int& bit) {
+  const int w = lr & 63, w2 = lr & 31;
+  word = (lr >> 6) * 2 + ((w2 >> 2) & 1);
+  bit = (w >> 5) * 16 + (w2 >> 3) * 4 + (w2 & 3);
+}
+
+// Record one row's bound factor for the epilogue (rv NaN: forced through,
+// ok false: skipped), the cosine term 1 / rv of its appends, and its flags
+// (words zeroed at the tile start, ordered by the K loop's barriers).
+template <int METRIC>
+__device__ __forceinline__ void filter_note_row(float* rinfo, float* rterm, uint32_t* flags,
+                                                int lr, float rv, bool ok) {
+  rinfo[lr] = ok ? rv : -1.f;
+  if constexpr (METRIC == 2) rterm[lr] = 1.f / rv;
+  int word, bit;
+  filter_row_bit(lr, word, bit);
+  if (!ok) atomicOr(&flags[8 + word], 1u << bit);
+  else if (rv != rv) atomicOr(&flags[word], 1u << bit);
+}
+
+// Epilogue of one tile: pass test per (row, query) — an fma, a subtraction
+// and a funnel shift that collects the sign of (product - threshold) (see
+// filter_query_table; extra passes only cost a rescored candidate); the
+// lane's passes over its 32 rows form a bit mask per query column, one
+// atomic per (lane, column) reserves their slots.  Forced rows (flag word 0..7)
+// always pass, skipped rows (8..15) never.
 template <int METRIC, int QT>
 __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], const float* rinfo,
+                                                const float* rterm, const uint32_t* flags,
                                                 const f32x4* qtab, const float2* qab,
                                                 const FilterArgs& a, int64_t q0, int64_t r0,
                                                 int rg, int qg, int h, int l32, int diag) {
@@ -340,22 +372,21 @@ __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], cons
     // row j of the lane (acc register j & 15 of row tile j >> 4) sits at a
     // compile-time offset from ri: row values are re-read from LDS where used
     auto roff = [](int j) { return (j >> 4) * 32 + (j & 3) + 8 * ((j & 15) >> 2); };
-    uint32_t fmask = 0u, smask = 0u;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const float rv = ri[roff(j)];
-      fmask |= (uint32_t)(rv != rv) << j;
-      smask |= (uint32_t)(rv < 0.f) << j;
-    }
+    const uint32_t fmask = flags[rg * 2 + h], smask = flags[8 + rg * 2 + h];
     uint32_t pm[QT];
 #pragma unroll
     for (int u = 0; u < QT; ++u) {
       const float2 ab = qab[qg * QT * 32 + u * 32 + l32];
-      uint32_t m = 0u;
+      // fail bits: sign of RN(x - t) is set exactly when x < t (x, t finite;
+      // RN never flips a sign, x == t gives +0); bit j enters last-in at
+      // bit 0, so j runs down
+      uint32_t fail = 0u;
 #pragma unroll
-      for (int j = 0; j < 32; ++j)
-        m |= (uint32_t)(acc[j >> 4][u][j & 15] >= fmaf(ab.x, ri[roff(j)], ab.y)) << j;
-      pm[u] = (diag & 1) ? 0u : ((m | fmask) & ~smask);
+      for (int j = 31; j >= 0; --j) {
+        const float t = fmaf(ab.x, ri[roff(j)], ab.y);
+        fail = __builtin_amdgcn_alignbit(fail, __float_as_uint(acc[j >> 4][u][j & 15] - t), 31);
+      }
+      pm[u] = (diag & 1) ? 0u : ((~fail | fmask) & ~smask);
       if (q0 + qg * QT * 32 + u * 32 + l32 >= a.nq) pm[u] = 0u;
     }
     uint32_t any = 0u;
@@ -378,8 +409,13 @@ __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], cons
       const float qc1 = qc[0], qc0 = qc[1], qA = qc[2], qB = qc[3];
       const bool fq = !(qA <= 3.4e38f);
       uint32_t p = pos[u];
+      // rows in groups of 4: a group no lane of the wave appends from is
+      // skipped with one wave-uniform branch (a few appends per wave and tile)
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
+      for (int g = 0; g < 8; ++g) {
+        if (__ballot(((pm[u] >> (4 * g)) & 0xfu) != 0u) == 0ull) continue;
+#pragma unroll
+      for (int j = 4 * g; j < 4 * g + 4; ++j) {
         if (!((pm[u] >> j) & 1u)) continue;
         const float rv = ri[roff(j)];
         const float x = acc[j >> 4][u][j & 15];
@@ -395,9 +431,9 @@ __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], cons
           lb = fmaf(x, qc1, -e);
           ub = fmaf(x, qc1, e);
         } else {
-          const float rterm = 1.f / rv;
-          const float dist = fmaf(x * rterm, qc1, 0.5f);
-          const float e = fmaf(qB, rterm, qA);
+          const float rt = rterm[lr0 + roff(j)];
+          const float dist = fmaf(x * rt, qc1, 0.5f);
+          const float e = fmaf(qB, rt, qA);
           lb = dist - e;
           ub = dist + e;
         }
@@ -417,33 +453,36 @@ __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], cons
         }
         ++p;
       }
+      }
     }
 }
 
-template <typename XT, int METRIC, bool IMG>
-__global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_kernel(FilterArgs a) {
-  static_assert(!IMG || sizeof(XT) == 2, "the filter image is fp16");
+// The tile loop of filter_kernel.  SF (store first): the wave stores chunk
+// c + 1 and issues its loads before it multiplies chunk c, instead of after.
+// Both orders are legal inside one barrier interval (the two touch different
+// LDS buffers); with FX_FILTER_SPLIT the second half of the workgroup (waves
+// fWaves/2.., each the SIMD partner of a first-half wave) takes the other
+// order, so one wave of a SIMD issues its MFMAs while its partner converts,
+// stores and loads, instead of both doing each phase together.
+template <typename XT, int METRIC, bool IMG, bool SF, typename Diag>
+__device__ __forceinline__ void filter_tiles(const FilterArgs& a, unsigned char* smem, int tid,
+                                             Diag diag) {
   using X = XPiece<XT>;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   FilterShared* sh = reinterpret_cast<FilterShared*>(smem);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lane = tid & 63, wid = tid >> 6;
   const int rg = wid % fRG, qg = wid / fRG;  // 64-row group, fQT*32-query group
   const int h = lane >> 5, l32 = lane & 31;
   const int64_t q0 = (int64_t)blockIdx.y * fBQ;
   const int nch = (a.d + fBK - 1) / fBK;
-#ifdef FX_FILTER_DIAG_BUILD
-  const int diag = a.diag;
-#else
-  constexpr int diag = 0;
-#endif
 
-  filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
-  // (the first tile's barriers order these writes before the epilogue reads)
-
-  for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x) {
+  int par = 0;  // tile parity: which rflags words this tile's epilogue reads
+  for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
     const int64_t tile = a.tile_start + ti * a.tile_stride;
     const int64_t r0 = tile * fBM;
     if (r0 >= a.n) continue;
+    // (last read by the epilogue two tiles back: every wave has passed the
+    // previous tile's barriers since)
+    if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;
 
     f32x16 acc[2][fQT];
 #pragma unroll
@@ -508,10 +547,15 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     // join and wait for every load in flight, draining the stream).
     auto step = [&](int c, FilterPre<XT>& p, auto buf) {
       constexpr int B = decltype(buf)::value;
-      if (!(diag & 4)) filter_compute<B>(acc, smem, o);
+      if constexpr (!SF) {
+        if (!(diag & 4)) filter_compute<B>(acc, smem, o);
+      }
       if (!(diag & 16)) filter_store<XT, B ^ 1, IMG>(p, pq, smem, o, sq, mx);
       filter_load_q(pq, ad, o, c + 2, diag);
       filter_load(p, ad, o, c + 3);
+      if constexpr (SF) {
+        if (!(diag & 4)) filter_compute<B>(acc, smem, o);
+      }
       __syncthreads();
     };
     using B0 = std::integral_constant<int, 0>;
@@ -563,7 +607,7 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
           rv = fmaxf(sqrtf(sqs[i]), 1e-12f);
         }
         if (!(sqs[i] <= 3.4e38f) || mx[i] >= 65520.f) rv = __builtin_nanf("");
-        sh->rinfo[lr] = ok ? rv : -1.f;
+        filter_note_row<METRIC>(sh->rinfo, sh->rterm, sh->rflags[par], lr, rv, ok);
       }
     }
     __syncthreads();
@@ -574,9 +618,34 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
       continue;
     }
 
-    filter_epilogue<METRIC, fQT>(acc, sh->rinfo, sh->qtab, sh->qab, a, q0, r0, rg, qg, h, l32,
-                                 diag);
+    filter_epilogue<METRIC, fQT>(acc, sh->rinfo, sh->rterm, sh->rflags[par], sh->qtab, sh->qab, a,
+                                 q0, r0, rg, qg, h, l32, diag);
   }
+}
+
+#ifndef FX_FILTER_SPLIT  // measured slower (6.48 vs 6.35 ms for configs[2], same box)
+#define FX_FILTER_SPLIT 0
+#endif
+
+template <typename XT, int METRIC, bool IMG>
+__global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_kernel(FilterArgs a) {
+  static_assert(!IMG || sizeof(XT) == 2, "the filter image is fp16");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  FilterShared* sh = reinterpret_cast<FilterShared*>(smem);
+  const int tid = threadIdx.x;
+  filter_query_table<METRIC>(a, (int64_t)blockIdx.y * fBQ, sh->qtab, sh->qab, tid, fThreads);
+  // (the first tile's barriers order these writes before the epilogue reads)
+#ifdef FX_FILTER_DIAG_BUILD
+  const int diag = a.diag;
+#else
+  constexpr int diag = 0;
+#endif
+  // wave-uniform role: the whole tile loop is instantiated per role, so the
+  // loop holds no join (both copies run the same count of barriers)
+  if (FX_FILTER_SPLIT && __builtin_amdgcn_readfirstlane(tid >> 6) >= fWaves / 2)
+    filter_tiles<XT, METRIC, IMG, true>(a, smem, tid, diag);
+  else
+    filter_tiles<XT, METRIC, IMG, false>(a, smem, tid, diag);
 }
 
 // ------------------------------------------------------------- LDS-DMA ring
@@ -614,7 +683,9 @@ struct Lay {
   static constexpr int qdma = (qblocks + kWaves - 1) / kWaves;
   static constexpr int ndma = xdma + qdma;
   static constexpr int rinfo = kStages * stage;
-  static constexpr int qtab = rinfo + kBM * 4;
+  static constexpr int rterm = rinfo + kBM * 4;
+  static constexpr int rflags = rterm + kBM * 4;  // [2][kRowFlagWords] by tile parity
+  static constexpr int qtab = rflags + 2 * kRowFlagWords * 4;
   static constexpr int qab = qtab + kBQ * 16;
   static constexpr int dummy = qab + kBQ * 8;
   static constexpr int total = dummy + 1024;
@@ -763,6 +834,8 @@ __global__ void __launch_bounds__(ring::kThreads, ring::kWaves / 4) ring_kernel(
   using L = Lay<XT>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* rinfo = reinterpret_cast<float*>(smem + L::rinfo);
+  float* rterm = reinterpret_cast<float*>(smem + L::rterm);
+  uint32_t* rflags = reinterpret_cast<uint32_t*>(smem + L::rflags);
   f32x4* qtab = reinterpret_cast<f32x4*>(smem + L::qtab);
   float2* qab = reinterpret_cast<float2*>(smem + L::qab);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -794,8 +867,11 @@ __global__ void __launch_bounds__(ring::kThreads, ring::kWaves / 4) ring_kernel(
     isb = isb == kStages - 1 ? 0 : isb + 1;
   }
   int sb = 0;  // stage buffer of the current step
-  for (; ti < a.num_tiles; ti += gridDim.x) {
+  int par = 0;
+  for (; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
     const int64_t r0 = tile_r0(ti);
+    uint32_t* flags = rflags + par * kRowFlagWords;
+    if (tid < kRowFlagWords) flags[tid] = 0u;  // (read two tiles back; barriers since)
     f32x16 acc[2][kQT];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -838,15 +914,15 @@ __global__ void __launch_bounds__(ring::kThreads, ring::kWaves / 4) ring_kernel(
             rv = fmaxf(sqrtf(sq[t]), 1e-12f);
           }
           if (!(sq[t] <= 3.4e38f) || of) rv = __builtin_nanf("");
-          rinfo[lr] = ok ? rv : -1.f;
+          filter_note_row<METRIC>(rinfo, rterm, flags, lr, rv, ok);
         }
       }
     }
     lds_sync();
     if (!(diag & 2)) {
       const int ol = (int)opaque(lane);  // keep the epilogue's lane math out of the chunk loop
-      filter_epilogue<METRIC, kQT>(acc, rinfo, qtab, qab, a, q0, r0, rg, qg, ol >> 5, ol & 31,
-                                   diag);
+      filter_epilogue<METRIC, kQT>(acc, rinfo, rterm, flags, qtab, qab, a, q0, r0, rg, qg, ol >> 5,
+                                   ol & 31, diag);
     }
   }
   // drain: the ring's last DMAs (empty descriptors past the end) must land

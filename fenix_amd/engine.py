@@ -298,7 +298,9 @@ class Engine:
                 or not _lib.filter_image_used(shard.n, shard.d, shard.dtype_id, nq, k, metric)):
             return None, None
         t = shard.data
-        if not t.is_contiguous():
+        # an unaligned corpus takes the scan's scalar-load variant, never the
+        # batched filter (fx_filter_image_used assumes 16-B aligned rows)
+        if not t.is_contiguous() or t.data_ptr() % 16 != 0:
             return None, None
         key = id(t)
         sig = (t.data_ptr(), tuple(t.shape), t._version)
