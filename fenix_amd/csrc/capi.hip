@@ -543,10 +543,10 @@ static int search_layout(const void* corpus, int dtype, int64_t n, int64_t d, in
 
 }  // extern "C"
 
-// a filter image applies to f32 rows through the register-staged filter, with
-// rows of whole 16-B pieces (d % 8 == 0)
+// a filter image applies to f32 rows through the fp16 filter, with rows of
+// whole 16-B pieces (d % 8 == 0)
 static bool image_applies(const SearchLayout& s, int dtype, int64_t d) {
-  return s.batched && s.batch.filter && dtype == FX_DTYPE_F32 && d % 8 == 0 && !filter_ring();
+  return s.batched && s.batch.filter && dtype == FX_DTYPE_F32 && d % 8 == 0;
 }
 
 static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,

@@ -119,7 +119,8 @@ struct FilterArgs {
   const float* rowinfo;   // [n] row sums of squares of the f32 rows when X is their fp16
                           // filter image (dtype F16), NaN = forced; null otherwise
   int diag;               // FX_FILTER_DIAG (profiling only): 1 no appends, 2 no epilogue,
-                          // 4 no MFMA, 8 no query loads, 16 no LDS stores
+                          // 4 no MFMA, 8 no query loads, 16 no LDS stores,
+                          // 32 no append atomics, 64 no append stores
 };
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream);
 // the LDS-DMA ring variant (knn_filter.hip ring_kernel) with FX_FILTER_RING=1

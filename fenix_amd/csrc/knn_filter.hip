@@ -68,6 +68,9 @@
 namespace fx {
 namespace FX_FILTER_IMPL {
 
+#if !defined(FX_FILTER_VARIANT) && defined(FX_Q256_WAVES)  // knob of this compilation only
+#define FX_FILTER_WAVES FX_Q256_WAVES
+#endif
 #ifndef FX_FILTER_WAVES
 #define FX_FILTER_WAVES 8   // waves per workgroup (two per SIMD)
 #endif
@@ -93,6 +96,13 @@ constexpr int fRG = fBM / 64;                   // 64-row groups (2 MFMA row til
 constexpr int fQG = fWaves / fRG;               // query groups
 constexpr int fQT = fBQ / fQG / 32;             // 32-query MFMA tiles per wave
 constexpr int fStages = FX_FILTER_STAGES;
+// Cross-tile prefetch (see filter_tiles): measured faster for the 64-query
+// tiles (16 queries, 10M x 768 image: 2.73 -> 2.65 ms), slower for the
+// 256-query ones (5.99 -> 6.1 ms BK 32, 6.35 ms BK 64: register pressure)
+#ifndef FX_FILTER_XPF
+#define FX_FILTER_XPF (FX_FILTER_BQ == 64)
+#endif
+constexpr bool kXpf = FX_FILTER_XPF;
 static_assert(fStages == 2, "the K loop alternates two register stages and two LDS buffers");
 constexpr int fQC = fBK / 8;                    // 16-B f16 pieces per query per chunk
 constexpr int fQP = fBQ * fQC / fThreads;       // Q pieces per thread per chunk
@@ -398,7 +408,12 @@ __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], cons
     for (int u = 0; u < QT; ++u) {
       pos[u] = 0u;
       const int64_t gq = q0 + qg * QT * 32 + u * 32 + l32;
-      if (pm[u] != 0u) pos[u] = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(pm[u]));
+      if (pm[u] != 0u) {
+        if ((diag & 32) && a.cand_ub != nullptr)  // profiling only (final phase): no atomic
+          pos[u] = (uint32_t)l32 * 64u;
+        else
+          pos[u] = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(pm[u]));
+      }
     }
 #pragma unroll
     for (int u = 0; u < QT; ++u) {
@@ -441,7 +456,7 @@ __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], cons
           lb = -__builtin_inff();
           ub = __builtin_nanf("");
         }
-        if (p < (uint32_t)a.cap) {
+        if (p < (uint32_t)a.cap && !((diag & 64) && a.cand_ub != nullptr)) {  // (64: profiling)
           const uint32_t grow = grow0 + (uint32_t)roff(j);
           const size_t slot = (size_t)gq * a.cap + p;
           if (a.cand_ub != nullptr) {
@@ -475,11 +490,58 @@ __device__ __forceinline__ void filter_tiles(const FilterArgs& a, unsigned char*
   const int64_t q0 = (int64_t)blockIdx.y * fBQ;
   const int nch = (a.d + fBK - 1) / fBK;
 
+  // the buffer descriptor of the X rows of the tile at row r0 (rows past n,
+  // or a tile past the end, read as zeros)
+  auto x_rsrc = [&](int64_t r0) {
+    int64_t rows = a.n - r0 < fBM ? a.n - r0 : fBM;
+    if (rows < 0) rows = 0;
+    const XT* xb = reinterpret_cast<const XT*>(a.X) + (rows > 0 ? r0 : 0) * (int64_t)a.d;
+    const uint64_t xp = reinterpret_cast<uint64_t>(xb);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xp >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)(rows * a.d * (int64_t)sizeof(XT)));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             nb, 0x00020000);
+  };
+  auto tile_r0 = [&](int64_t ti) { return (a.tile_start + ti * a.tile_stride) * fBM; };
+  FilterAddr ad;
+  {
+    const uint16_t* qb = a.Qh + q0 * 32;
+    const uint64_t qp = reinterpret_cast<uint64_t>(qb);
+    const uint32_t qlo = __builtin_amdgcn_readfirstlane((uint32_t)qp);
+    const uint32_t qhi = __builtin_amdgcn_readfirstlane((uint32_t)(qp >> 32));
+    const int qnb = __builtin_amdgcn_readfirstlane(
+        (int)(((int64_t)(a.dq / 32 - 1) * a.qstride + fBQ) * 64));
+    ad.qr = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)qhi << 32) | qlo), 0, qnb, 0x00020000);
+    ad.d = a.d;
+    ad.xs = (uint32_t)(fThreads / X::C) * (uint32_t)a.d * (uint32_t)sizeof(XT);
+    ad.qs = (uint32_t)(fThreads / fQC) * 64u;
+    ad.qb = (uint32_t)a.qstride * 64u;
+    ad.dq = a.dq;
+  }
+
+  // Two register stages: chunks c + 2 and c + 3 of X are in flight while
+  // chunk c is multiplied (stage j % 2 holds chunk j), the query tile one
+  // chunk ahead.  Loads are issued unconditionally (chunks past the row end
+  // read as zeros through the descriptor bounds): a load under a branch
+  // makes the compiler wait for it where the branch joins.  With kXpf a
+  // tile's first two X chunks and first query chunk are issued before the
+  // previous tile's epilogue (the stages are free by then), so they stream
+  // in while it runs.
+  FilterPre<XT> pf[2];
+  FilterPreQ pq;
+  int64_t ti = blockIdx.x;
+  if constexpr (kXpf) {
+    ad.xr = x_rsrc(tile_r0(ti));
+    const FilterOff o = filter_offsets<XT>(opaque(tid), ad);
+    filter_load_q(pq, ad, o, 0, diag);
+    filter_load(pf[0], ad, o, 0);
+    filter_load(pf[1], ad, o, 1);
+  }
   int par = 0;  // tile parity: which rflags words this tile's epilogue reads
-  for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
-    const int64_t tile = a.tile_start + ti * a.tile_stride;
-    const int64_t r0 = tile * fBM;
-    if (r0 >= a.n) continue;
+  for (; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
+    const int64_t r0 = tile_r0(ti);
     // (last read by the epilogue two tiles back: every wave has passed the
     // previous tile's barriers since)
     if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;
@@ -497,42 +559,13 @@ __device__ __forceinline__ void filter_tiles(const FilterArgs& a, unsigned char*
       mx[i] = 0.f;
     }
 
-    const int64_t rows = a.n - r0 < fBM ? a.n - r0 : fBM;
-    FilterAddr ad;
-    {
-      const XT* xb = reinterpret_cast<const XT*>(a.X) + r0 * (int64_t)a.d;
-      const uint64_t xp = reinterpret_cast<uint64_t>(xb);
-      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xp);
-      const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xp >> 32));
-      const int nb = __builtin_amdgcn_readfirstlane((int)(rows * a.d * (int64_t)sizeof(XT)));
-      ad.xr = __builtin_amdgcn_make_buffer_rsrc(
-          reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
-      const uint16_t* qb = a.Qh + q0 * 32;
-      const uint64_t qp = reinterpret_cast<uint64_t>(qb);
-      const uint32_t qlo = __builtin_amdgcn_readfirstlane((uint32_t)qp);
-      const uint32_t qhi = __builtin_amdgcn_readfirstlane((uint32_t)(qp >> 32));
-      const int qnb = __builtin_amdgcn_readfirstlane(
-          (int)(((int64_t)(a.dq / 32 - 1) * a.qstride + fBQ) * 64));
-      ad.qr = __builtin_amdgcn_make_buffer_rsrc(
-          reinterpret_cast<void*>(((uint64_t)qhi << 32) | qlo), 0, qnb, 0x00020000);
-      ad.d = a.d;
-      ad.xs = (uint32_t)(fThreads / X::C) * (uint32_t)a.d * (uint32_t)sizeof(XT);
-      ad.qs = (uint32_t)(fThreads / fQC) * 64u;
-      ad.qb = (uint32_t)a.qstride * 64u;
-      ad.dq = a.dq;
-    }
+    ad.xr = x_rsrc(r0);
     const FilterOff o = filter_offsets<XT>(opaque(tid), ad);
-
-    // Two register stages: chunks c + 2 and c + 3 of X are in flight while
-    // chunk c is multiplied (stage j % 2 holds chunk j), the query tile one
-    // chunk ahead.  Loads are issued unconditionally (chunks past the row end
-    // read as zeros through the descriptor bounds): a load under a branch
-    // makes the compiler wait for it where the branch joins.
-    FilterPre<XT> pf[2];
-    FilterPreQ pq;
-    filter_load_q(pq, ad, o, 0, diag);
-    filter_load(pf[0], ad, o, 0);
-    filter_load(pf[1], ad, o, 1);
+    if constexpr (!kXpf) {
+      filter_load_q(pq, ad, o, 0, diag);
+      filter_load(pf[0], ad, o, 0);
+      filter_load(pf[1], ad, o, 1);
+    }
     filter_store<XT, 0, IMG>(pf[0], pq, smem, o, sq, mx);
     // Q one chunk ahead, issued before the X load of the same step: vmcnt
     // retires loads in issue order, so waiting for Q(c + 1) at step c waits
@@ -571,8 +604,30 @@ __device__ __forceinline__ void filter_tiles(const FilterArgs& a, unsigned char*
     const bool two = c + 1 < nch;
     if (two && !(diag & 16)) filter_store<XT, 1, IMG>(pf[1], pq, smem, o, sq, mx);
     __syncthreads();
+    // kXpf: the rows' image sums and mask words for the epilogue, issued
+    // before the last chunks' MFMAs and the next tile's loads, so they are in
+    // when it starts without waiting for those
+    float img_sq[X::P];
+    uint32_t mword[X::P];
+    if constexpr (kXpf) {
+#pragma unroll
+      for (int i = 0; i < X::P; ++i) {
+        const int lr = (i * fThreads + tid) / X::C;
+        const int64_t row = r0 + lr < a.n ? r0 + lr : a.n - 1;
+        if constexpr (IMG) img_sq[i] = a.rowinfo[row];
+        mword[i] = a.mask != nullptr ? a.mask[row >> 5] : ~0u;
+      }
+    }
     if (!(diag & 4)) filter_compute<0>(acc, smem, o);
     if (two && !(diag & 4)) filter_compute<1>(acc, smem, o);
+    if constexpr (kXpf) {  // the next tile's first chunks (past the end: an empty descriptor)
+      const int64_t tn = ti + gridDim.x;
+      ad.xr = x_rsrc(tn < a.num_tiles ? tile_r0(tn) : a.n);
+      const FilterOff on = filter_offsets<XT>(opaque(tid), ad);
+      filter_load_q(pq, ad, on, 0, diag);
+      filter_load(pf[0], ad, on, 0);
+      filter_load(pf[1], ad, on, 1);
+    }
 
     // per-row value rv from |x|^2 (the fRowLanes lanes of a row hold partials;
     // IMG: the f32 row's, precomputed): cosine max(|x|, 1e-12), IP |x|, L2
@@ -596,8 +651,13 @@ __device__ __forceinline__ void filter_tiles(const FilterArgs& a, unsigned char*
         const int lr = (i * fThreads + tid) / X::C;
         const int64_t row = r0 + lr;
         bool ok = row < a.n;
-        if constexpr (IMG) sqs[i] = ok ? a.rowinfo[row] : 0.f;
-        if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
+        if constexpr (kXpf) {
+          if constexpr (IMG) sqs[i] = ok ? img_sq[i] : 0.f;
+          if (ok) ok = (mword[i] >> (row & 31)) & 1u;
+        } else {
+          if constexpr (IMG) sqs[i] = ok ? a.rowinfo[row] : 0.f;
+          if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
+        }
         float rv;
         if constexpr (METRIC == 0) {
           rv = sqs[i];
@@ -760,7 +820,7 @@ __device__ __forceinline__ void ring_issue(unsigned char* smem, const FilterArgs
 // kv = d - (first k of the chunk): elements at k >= d are zeroed (the DMA of a
 // piece past the row end is dropped, leaving stale LDS there; the query tile
 // is zero-padded, but the row sums must not see it).
-template <typename XT>
+template <typename XT, bool IMG>
 __device__ __forceinline__ void ring_compute(f32x16 (&acc)[2][kQT], const unsigned char* st,
                                              int rg, int qg, int l32, int h, int kv,
                                              float (&sq)[2], uint32_t& ovf) {
@@ -795,7 +855,7 @@ __device__ __forceinline__ void ring_compute(f32x16 (&acc)[2][kQT], const unsign
         const int p = 2 * s + h;
         av[t] = *reinterpret_cast<const f16x8*>(st + R * L::xrow + ((p ^ ((R >> 2) & 3)) * 16));
         if (kf >= kv) av[t] = f16x8(0);
-        if (qg == 0) {
+        if (!IMG && qg == 0) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) sq[t] = fmaf((float)av[t][e], (float)av[t][e], sq[t]);
         }
@@ -828,7 +888,8 @@ __device__ __forceinline__ void lds_sync() {
 }
 }  // namespace ring
 
-template <typename XT, int METRIC>
+// IMG: the rows are an f32 corpus's fp16 filter image (row sums from rowinfo)
+template <typename XT, int METRIC, bool IMG>
 __global__ void __launch_bounds__(ring::kThreads, ring::kWaves / 4) ring_kernel(FilterArgs a) {
   using namespace ring;
   using L = Lay<XT>;
@@ -889,7 +950,7 @@ __global__ void __launch_bounds__(ring::kThreads, ring::kWaves / 4) ring_kernel(
       isb = isb == kStages - 1 ? 0 : isb + 1;
       if (!(diag & 4)) {
         const int ol = (int)opaque(lane);
-        ring_compute<XT>(acc, smem + sb * L::stage, rg, qg, ol & 31, ol >> 5, a.d - c * kBK, sq,
+        ring_compute<XT, IMG>(acc, smem + sb * L::stage, rg, qg, ol & 31, ol >> 5, a.d - c * kBK, sq,
                          ovf);
       }
       sb = sb == kStages - 1 ? 0 : sb + 1;
@@ -904,6 +965,7 @@ __global__ void __launch_bounds__(ring::kThreads, ring::kWaves / 4) ring_kernel(
           const int lr = rg * 64 + t * 32 + l32;
           const int64_t row = r0 + lr;
           bool ok = row < a.n;
+          if constexpr (IMG) sq[t] = ok ? a.rowinfo[row] : 0.f;
           if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
           float rv;
           if constexpr (METRIC == 0) {
@@ -930,12 +992,12 @@ __global__ void __launch_bounds__(ring::kThreads, ring::kWaves / 4) ring_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <typename XT>
+template <typename XT, bool IMG = false>
 static int launch_ring(const FilterArgs& a, int metric, hipStream_t stream) {
   const size_t smem = ring::Lay<XT>::total;
-  const void* fn = metric == FX_METRIC_COS ? (const void*)ring_kernel<XT, 2>
-                   : metric == FX_METRIC_IP ? (const void*)ring_kernel<XT, 1>
-                                            : (const void*)ring_kernel<XT, 0>;
+  const void* fn = metric == FX_METRIC_COS ? (const void*)ring_kernel<XT, 2, IMG>
+                   : metric == FX_METRIC_IP ? (const void*)ring_kernel<XT, 1, IMG>
+                                            : (const void*)ring_kernel<XT, 0, IMG>;
   if (int rc = allow_lds(fn)) return rc;
   int cus = 0;
   int rc = device_cus(&cus);
@@ -967,12 +1029,16 @@ static int launch_ring(const FilterArgs& a, int metric, hipStream_t stream) {
 int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.num_tiles <= 0) return FX_OK;
   const bool f16 = a.dtype == FX_DTYPE_F16;
-  if (filter_ring() && a.rowinfo != nullptr) {
-    set_error("filter: the LDS-DMA ring does not read a filter image");
-    return FX_EUNSUPPORTED;
+  if (filter_ring()) {
+    if (a.rowinfo != nullptr) {
+      if (!f16) {
+        set_error("filter: a filter image is fp16");
+        return FX_EINVAL;
+      }
+      return launch_ring<_Float16, true>(a, metric, stream);
+    }
+    return f16 ? launch_ring<_Float16>(a, metric, stream) : launch_ring<float>(a, metric, stream);
   }
-  if (filter_ring()) return f16 ? launch_ring<_Float16>(a, metric, stream)
-                                : launch_ring<float>(a, metric, stream);
   const size_t smem = sizeof(FilterShared);
   // (the 256-query compilation serves f32 rows, h256 fp16 rows, q64 both)
 #if FX_FILTER_ROWS & 1

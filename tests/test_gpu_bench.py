@@ -50,3 +50,22 @@ def test_bench_cpu_baseline_fields():
                     "--cpu-seconds", "0.5")
     cpu = rec["cpu_baseline"]
     assert cpu["kind"] in ("port", "reference") and cpu["cores"] >= 1 and cpu["value"] > 0
+
+
+def test_bench_rccl_path_one_rank():
+    """The N > 1 path of bench.py (RCCL process group, all-gather of the per-rank
+    top-k, merge, barriers, max-over-ranks all-reduce) launched the way the
+    driver launches it, with one rank: the one-GPU box runs every RCCL call
+    the 8-GPU scaling run makes."""
+    env = dict(os.environ, FENIX_AMD_BENCH_DIST="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", "29531", os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--rows", "300000", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["config"]["parallelism"] == "row-shard x1 + RCCL all-gather"
+    assert rec["n_gpus"] == 1 and rec["value"] > 0
