@@ -81,6 +81,9 @@
 #ifndef FX_Q8DMA_U
 #define FX_Q8DMA_U 1
 #endif
+#ifndef FX_Q8DMA_AUX  // cache policy of the code stream's LDS-DMA loads (2: nontemporal)
+#define FX_Q8DMA_AUX 2
+#endif
 #ifndef FX_Q8DMA_STAGES
 #define FX_Q8DMA_STAGES 3
 #endif
@@ -547,7 +550,7 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
             const void* g = reinterpret_cast<const T*>(a.X) + row * (int64_t)a.d + (sl < S ? sl : 0) * 16;
             __builtin_amdgcn_global_load_lds(
                 g, (__attribute__((address_space(3))) void*)(ring + j * kTileBytes + (u * L + cc) * 1024),
-                16, 0, 0);
+                16, 0, FX_Q8DMA_AUX);
           }
         }
       }
@@ -564,7 +567,7 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
             const void* g = reinterpret_cast<const T*>(a.X) + row * (int64_t)a.d + (sl < S ? sl : 0) * 16;
             __builtin_amdgcn_global_load_lds(
                 g, (__attribute__((address_space(3))) void*)(ring + slot_n * kTileBytes + (u * L + cc) * 1024),
-                16, 0, 0);
+                16, 0, FX_Q8DMA_AUX);
           }
         }
       }
