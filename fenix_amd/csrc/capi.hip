@@ -641,7 +641,8 @@ int fx_filter_image_bytes(int64_t n, int64_t d, size_t* image_bytes, size_t* row
               (long long)d);
     return FX_EUNSUPPORTED;
   }
-  *image_bytes = (size_t)n * (size_t)d * 2;
+  *image_bytes = image_tiled() ? (size_t)((n + 31) / 32) * (size_t)((d + 15) / 16) * 1024
+                               : (size_t)n * (size_t)d * 2;
   *rowinfo_bytes = (size_t)n * 4;
   return FX_OK;
 }

@@ -126,6 +126,9 @@ int launch_filter(const FilterArgs& a, int metric, hipStream_t stream);
 // the LDS-DMA ring variant (knn_filter.hip ring_kernel) with FX_FILTER_RING=1
 // (the register-staged kernel otherwise)
 bool filter_ring();
+// filter images in MFMA fragment order (knn_filter.hip filter_img2_kernel);
+// FX_IMAGE_TILED=0: row-major
+bool image_tiled();
 int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
                  uint16_t* Qh, float* qinfo, hipStream_t stream);
 int filter_tile_rows(int dtype);

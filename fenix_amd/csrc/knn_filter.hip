@@ -127,8 +127,9 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // Per-tile row flags for the epilogue, by tile parity: [forced | skipped][8]
 // 32-bit masks, one per (64-row group, lane half) in the bit order of the
-// lane's 32 accumulator rows (filter_row_bit)
-constexpr int kRowFlagWords = 2 * 8;
+// lane's accumulator rows (filter_row_bit); up to 16 (row group, lane half)
+// words per kind: 32-row groups (the tiled-image kernel) or 64-row groups
+constexpr int kRowFlagWords = 2 * 16;
 static_assert(fBM <= 256, "row flag words: (64-row group, lane half) <= 8");
 struct FilterShared {
   _Float16 xs[2][fBM * fLds];
@@ -341,48 +342,52 @@ __device__ __forceinline__ void filter_query_table(const FilterArgs& a, int64_t 
   }
 }
 
-// Where local row lr of a 256-row tile sits in the epilogue's masks: the
-// word of its (64-row group, lane half) and its bit there, j with
-// lr = 64 rg + 4 h + roff(j) (filter_epilogue).
+// Where local row lr of a 256-row tile sits in the epilogue's masks when a
+// wave owns RT 32-row MFMA tiles: the word of its (32 RT-row group, lane
+// half) and its bit there, j with lr = 32 RT rg + 4 h + roff(j)
+// (filter_epilogue).
+template <int RT>
 __device__ __forceinline__ void filter_row_bit(int lr, int& word, int& bit) {
-  const int w = lr & 63, w2 = lr & 31;
-  word = (lr >> 6) * 2 + ((w2 >> 2) & 1);
+  const int w = lr % (32 * RT), w2 = lr & 31;
+  word = (lr / (32 * RT)) * 2 + ((w2 >> 2) & 1);
   bit = (w >> 5) * 16 + (w2 >> 3) * 4 + (w2 & 3);
 }
 
 // Record one row's bound factor for the epilogue (rv NaN: forced through,
 // ok false: skipped), the cosine term 1 / rv of its appends, and its flags
 // (words zeroed at the tile start, ordered by the K loop's barriers).
-template <int METRIC>
+template <int METRIC, int RT = 2>
 __device__ __forceinline__ void filter_note_row(float* rinfo, float* rterm, uint32_t* flags,
                                                 int lr, float rv, bool ok) {
   rinfo[lr] = ok ? rv : -1.f;
   if constexpr (METRIC == 2) rterm[lr] = 1.f / rv;
   int word, bit;
-  filter_row_bit(lr, word, bit);
-  if (!ok) atomicOr(&flags[8 + word], 1u << bit);
+  filter_row_bit<RT>(lr, word, bit);
+  if (!ok) atomicOr(&flags[16 + word], 1u << bit);
   else if (rv != rv) atomicOr(&flags[word], 1u << bit);
 }
 
 // Epilogue of one tile: pass test per (row, query) — an fma, a subtraction
 // and a funnel shift that collects the sign of (product - threshold) (see
 // filter_query_table; extra passes only cost a rescored candidate); the
-// lane's passes over its 32 rows form a bit mask per query column, one
-// atomic per (lane, column) reserves their slots.  Forced rows (flag word 0..7)
-// always pass, skipped rows (8..15) never.
-template <int METRIC, int QT>
-__device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], const float* rinfo,
+// lane's passes over its 16 RT rows form a bit mask per query column, one
+// atomic per (lane, column) reserves their slots.  Forced rows (flag words
+// 0..15) always pass, skipped rows (16..31) never.
+template <int METRIC, int QT, int RT = 2>
+__device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[RT][QT], const float* rinfo,
                                                 const float* rterm, const uint32_t* flags,
                                                 const f32x4* qtab, const float2* qab,
                                                 const FilterArgs& a, int64_t q0, int64_t r0,
                                                 int rg, int qg, int h, int l32, int diag) {
-    const int lr0 = rg * 64 + 4 * h;
+    constexpr int NR = 16 * RT;  // rows per lane
+    constexpr uint32_t kAll = NR == 32 ? ~0u : (1u << NR) - 1u;
+    const int lr0 = rg * 32 * RT + 4 * h;
     const float* ri = rinfo + lr0;
     const uint32_t grow0 = (uint32_t)(a.row_base + r0 + lr0);
     // row j of the lane (acc register j & 15 of row tile j >> 4) sits at a
     // compile-time offset from ri: row values are re-read from LDS where used
     auto roff = [](int j) { return (j >> 4) * 32 + (j & 3) + 8 * ((j & 15) >> 2); };
-    const uint32_t fmask = flags[rg * 2 + h], smask = flags[8 + rg * 2 + h];
+    const uint32_t fmask = flags[rg * 2 + h], smask = flags[16 + rg * 2 + h];
     uint32_t pm[QT];
 #pragma unroll
     for (int u = 0; u < QT; ++u) {
@@ -392,11 +397,11 @@ __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], cons
       // bit 0, so j runs down
       uint32_t fail = 0u;
 #pragma unroll
-      for (int j = 31; j >= 0; --j) {
+      for (int j = NR - 1; j >= 0; --j) {
         const float t = fmaf(ab.x, ri[roff(j)], ab.y);
         fail = __builtin_amdgcn_alignbit(fail, __float_as_uint(acc[j >> 4][u][j & 15] - t), 31);
       }
-      pm[u] = (diag & 1) ? 0u : ((~fail | fmask) & ~smask);
+      pm[u] = (diag & 1) ? 0u : ((~fail | fmask) & ~smask & kAll);
       if (q0 + qg * QT * 32 + u * 32 + l32 >= a.nq) pm[u] = 0u;
     }
     uint32_t any = 0u;
@@ -427,7 +432,7 @@ __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[2][QT], cons
       // rows in groups of 4: a group no lane of the wave appends from is
       // skipped with one wave-uniform branch (a few appends per wave and tile)
 #pragma unroll
-      for (int g = 0; g < 8; ++g) {
+      for (int g = 0; g < NR / 4; ++g) {
         if (__ballot(((pm[u] >> (4 * g)) & 0xfu) != 0u) == 0ull) continue;
 #pragma unroll
       for (int j = 4 * g; j < 4 * g + 4; ++j) {
@@ -681,6 +686,210 @@ __device__ __forceinline__ void filter_tiles(const FilterArgs& a, unsigned char*
     filter_epilogue<METRIC, fQT>(acc, sh->rinfo, sh->rterm, sh->rflags[par], sh->qtab, sh->qab, a,
                                  q0, r0, rg, qg, h, l32, diag);
   }
+}
+
+// ------------------------------------------------------ tiled filter image
+//
+// The fp16 image of an f32 corpus in MFMA fragment order (FX_IMAGE_TILED,
+// default on), [ceil(n / 32) row tiles][ceil(d / 16) k-steps][64 lanes][8
+// halves]: lane l holds row 32 t + l % 32, components 16 s + 8 (l / 32) ..
+// + 7, i.e. one v_mfma_f32_32x32x16_f16 A operand, one contiguous KB per wave
+// load.  Each of the 8 waves owns one 32-row tile of the 256-row tile against
+// all the queries and loads its A fragments straight into registers (two
+// chunks ahead); only the query tile goes through LDS.
+struct Img2Shared {
+  _Float16 qs[2][fBQ * fLds];
+  float rinfo[fBM];
+  float rterm[fBM];
+  uint32_t rflags[2][kRowFlagWords];
+  f32x4 qtab[fBQ];
+  float2 qab[fBQ];
+};
+constexpr int kI2QT = fBQ / 32;  // query tiles per wave (every query)
+constexpr int kI2KS = fBK / 16;  // k-steps per chunk
+static_assert(fWaves * 32 == fBM, "tiled image: one 32-row tile per wave");
+
+template <int METRIC>
+__global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(FilterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Img2Shared* sh = reinterpret_cast<Img2Shared*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, l32 = lane & 31;
+  const int64_t q0 = (int64_t)blockIdx.y * fBQ;
+  const int nch = (a.d + fBK - 1) / fBK;
+  const int ksteps = (a.d + 15) / 16;
+  const int64_t ntile32 = (a.n + 31) / 32;
+#ifdef FX_FILTER_DIAG_BUILD
+  const int diag = a.diag;
+#else
+  constexpr int diag = 0;
+#endif
+  filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
+
+  FilterAddr ad;  // the query tile (as filter_tiles)
+  {
+    const uint16_t* qb = a.Qh + q0 * 32;
+    const uint64_t qp = reinterpret_cast<uint64_t>(qb);
+    const uint32_t qlo = __builtin_amdgcn_readfirstlane((uint32_t)qp);
+    const uint32_t qhi = __builtin_amdgcn_readfirstlane((uint32_t)(qp >> 32));
+    const int qnb = __builtin_amdgcn_readfirstlane(
+        (int)(((int64_t)(a.dq / 32 - 1) * a.qstride + fBQ) * 64));
+    ad.qr = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)qhi << 32) | qlo), 0, qnb, 0x00020000);
+    ad.d = a.d;
+    ad.xs = 0;
+    ad.qs = (uint32_t)(fThreads / fQC) * 64u;
+    ad.qb = (uint32_t)a.qstride * 64u;
+    ad.dq = a.dq;
+  }
+  FilterOff o = {};
+  {
+    const unsigned t = opaque(tid);
+    o.qg = (t / fQC) * 64 + (t % fQC) % 4 * 16 + (t % fQC) / 4 * ad.qb;
+  }
+  const uint32_t qw = ((tid / fQC) * fLds + (tid % fQC) * 8) * 2;  // this thread's Q stores
+  const uint32_t qr = (l32 * fLds + 8 * h) * 2;                    // this lane's B fragments
+
+  auto store_q = [&](const FilterPreQ& pq, auto buf) {
+    constexpr int B = decltype(buf)::value;
+#pragma unroll
+    for (int i = 0; i < fQP; ++i)
+      lds_at<i32x4>(smem, B * kQB + qw + i * (fThreads / fQC) * fLds * 2) = pq.q[i];
+  };
+  typedef f16x8 XA[kI2KS];
+  int par = 0;
+  for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
+    const int64_t r0 = (a.tile_start + ti * a.tile_stride) * fBM;
+    if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;
+    // this wave's 32-row tile: its k-steps, one KB each (a tile past the end
+    // reads zeros through the descriptor size)
+    __amdgpu_buffer_rsrc_t xr;
+    {
+      const int64_t t32 = r0 / 32 + wid;
+      const int64_t live = t32 < ntile32 ? 1 : 0;
+      const unsigned char* base = reinterpret_cast<const unsigned char*>(a.X) +
+                                  (live ? t32 : 0) * (int64_t)ksteps * 1024;
+      const uint64_t xp = reinterpret_cast<uint64_t>(base);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xp);
+      const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xp >> 32));
+      const int nb = __builtin_amdgcn_readfirstlane((int)(live * ksteps * 1024));
+      xr = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             nb, 0x00020000);
+    }
+    const uint32_t xl = (uint32_t)opaque(lane) * 16u;
+    auto load_x = [&](XA& xa, int c) {
+#pragma unroll
+      for (int s = 0; s < kI2KS; ++s) {
+        const int ks = c * kI2KS + s;  // wave-uniform: past the row end reads zeros
+        const uint32_t off = ks < ksteps ? xl : 0x7fff0000u;
+        xa[s] = __builtin_bit_cast(
+            f16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, ks * 1024, 2 /* nt */));
+      }
+    };
+    f32x16 acc[1][kI2QT];
+#pragma unroll
+    for (int u = 0; u < kI2QT; ++u) acc[0][u] = f32x16(0.f);
+    auto compute = [&](const XA& xa, auto buf) {
+      constexpr int B = decltype(buf)::value;
+#pragma unroll
+      for (int s = 0; s < kI2KS; ++s) {
+#pragma unroll
+        for (int u = 0; u < kI2QT; ++u) {
+          const f16x8 bv = lds_at<f16x8>(smem, B * kQB + qr + (u * 32 * fLds + 16 * s) * 2);
+          acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bv, acc[0][u], 0, 0, 0);
+        }
+      }
+    };
+    XA xa0, xa1;
+    FilterPreQ pq;
+    filter_load_q(pq, ad, o, 0, diag);
+    load_x(xa0, 0);
+    load_x(xa1, 1);
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    store_q(pq, B0{});
+    filter_load_q(pq, ad, o, 1, diag);
+    __syncthreads();
+    // step c: multiply chunk c (registers xa[c & 1], query buffer c & 1),
+    // store query chunk c + 1, load query chunk c + 2 and rows chunk c + 2
+    auto step = [&](int c, XA& xa, auto buf) {
+      constexpr int B = decltype(buf)::value;
+      compute(xa, buf);
+      store_q(pq, std::integral_constant<int, B ^ 1>{});
+      filter_load_q(pq, ad, o, c + 2, diag);
+      load_x(xa, c + 2);
+      __syncthreads();
+    };
+    int c = 0;
+    for (; c + 2 < nch; c += 2) {
+      step(c, xa0, B0{});
+      step(c + 1, xa1, B1{});
+    }
+    const bool two = c + 1 < nch;
+    if (two) store_q(pq, B1{});
+    __syncthreads();
+    compute(xa0, B0{});
+    if (two) compute(xa1, B1{});
+
+    if (tid < fBM) {  // one thread per row: bound factor, flags
+      const int lr = tid;
+      const int64_t row = r0 + lr;
+      bool ok = row < a.n;
+      const float s = ok ? a.rowinfo[row] : 0.f;
+      if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
+      float rv;
+      if constexpr (METRIC == 0) {
+        rv = s;
+      } else if constexpr (METRIC == 1) {
+        rv = sqrtf(s);
+      } else {
+        rv = fmaxf(sqrtf(s), 1e-12f);
+      }
+      if (!(s <= 3.4e38f)) rv = __builtin_nanf("");
+      filter_note_row<METRIC, 1>(sh->rinfo, sh->rterm, sh->rflags[par], lr, rv, ok);
+    }
+    __syncthreads();
+    if (diag & 2) {
+      if (acc[0][0][0] == 1.2345f) a.count[0] = 7;
+      continue;
+    }
+    filter_epilogue<METRIC, kI2QT, 1>(acc, sh->rinfo, sh->rterm, sh->rflags[par], sh->qtab,
+                                      sh->qab, a, q0, r0, wid, 0, h, l32, diag);
+  }
+}
+
+static int launch_img2(const FilterArgs& a, int metric, hipStream_t stream) {
+  const size_t smem = sizeof(Img2Shared);
+  const void* fn = metric == FX_METRIC_COS ? (const void*)filter_img2_kernel<2>
+                   : metric == FX_METRIC_IP ? (const void*)filter_img2_kernel<1>
+                                            : (const void*)filter_img2_kernel<0>;
+  if (int rc = allow_lds(fn)) return rc;
+  int cus = 0;
+  int rc = device_cus(&cus);
+  if (rc) return rc;
+  const int64_t qtiles = (a.nq + fBQ - 1) / fBQ;
+  int64_t bx = cus;
+  if (bx > a.num_tiles) bx = a.num_tiles;
+  for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
+    FilterArgs b = a;
+    const int64_t yn = (qtiles - y0) < 65535 ? (qtiles - y0) : 65535;
+    b.Qh = a.Qh + y0 * fBQ * 32;
+    b.qinfo = a.qinfo + y0 * fBQ * 4;
+    b.thr = a.thr + y0 * fBQ;
+    b.count = a.count + y0 * fBQ * kCountStride;
+    b.cand = a.cand + y0 * fBQ * (int64_t)a.cap;
+    if (a.cand_ub) b.cand_ub = a.cand_ub + y0 * fBQ * (int64_t)a.cap;
+    b.nq = a.nq - y0 * fBQ;
+    void* args[] = {(void*)&b};
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(fThreads), args,
+                                   smem, stream);
+    if (e != hipSuccess) {
+      set_error("filter_img2_kernel launch: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+  }
+  return check_launch("filter_img2_kernel");
 }
 
 #ifndef FX_FILTER_SPLIT  // measured slower (6.48 vs 6.35 ms for configs[2], same box)
@@ -1029,6 +1238,14 @@ static int launch_ring(const FilterArgs& a, int metric, hipStream_t stream) {
 int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.num_tiles <= 0) return FX_OK;
   const bool f16 = a.dtype == FX_DTYPE_F16;
+  if (a.rowinfo != nullptr && image_tiled()) {  // the image in MFMA fragment order
+#if FX_FILTER_ROWS & 2
+    return launch_img2(a, metric, stream);
+#else
+    set_error("filter: the tiled image is not compiled into this variant");
+    return FX_EUNSUPPORTED;
+#endif
+  }
   if (filter_ring()) {
     if (a.rowinfo != nullptr) {
       if (!f16) {
@@ -1106,6 +1323,15 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_
 // The register-staged kernel by default (measured faster for both row types:
 // 8.5 vs 10.1 ms for configs[2]; see DESIGN.md for fp16); FX_FILTER_RING=1
 // selects the LDS-DMA ring.
+// Filter images in MFMA fragment order (filter_img2_kernel) by default;
+// FX_IMAGE_TILED=0 selects row-major images (the register-staged kernels'
+// IMG path).  Read when an image is built and when it is searched: both must
+// happen under the same setting.
+bool image_tiled() {
+  const char* env = getenv("FX_IMAGE_TILED");
+  return env == nullptr || atoi(env) != 0;
+}
+
 bool filter_ring() {
   const char* env = getenv("FX_FILTER_RING");
   return env != nullptr && atoi(env) != 0;
@@ -1211,16 +1437,24 @@ typedef float img_f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 img_f16x4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256) image_kernel(const float* __restrict__ X, int64_t n, int d,
                                                     _Float16* __restrict__ img,
-                                                    float* __restrict__ rowinfo) {
+                                                    float* __restrict__ rowinfo, bool tiled) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t ksteps = (d + 15) / 16;
   for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += nw) {
     const img_f32x4* xr = reinterpret_cast<const img_f32x4*>(X + r * d);
     img_f16x4* ir = reinterpret_cast<img_f16x4*>(img + r * d);
     float s = 0.f, m = 0.f;
     for (int i = lane; i < d / 4; i += 64) {
       const img_f32x4 v = __builtin_nontemporal_load(xr + i);
-      ir[i] = __builtin_convertvector(v, img_f16x4);
+      if (tiled) {  // components 4i..4i+3 of row r at their MFMA-fragment position
+        const int k = 4 * i;
+        const int64_t at =
+            (((r >> 5) * ksteps + (k >> 4)) * 64 + (r & 31) + 32 * ((k & 15) >> 3)) * 8 + (k & 7);
+        *reinterpret_cast<img_f16x4*>(img + at) = __builtin_convertvector(v, img_f16x4);
+      } else {
+        ir[i] = __builtin_convertvector(v, img_f16x4);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         s = fmaf(v[e], v[e], s);
@@ -1244,8 +1478,16 @@ int launch_image(const float* X, int64_t n, int d, void* img, float* rowinfo,
   if (rc) return rc;
   int64_t blocks = (n + 3) / 4;
   if (blocks > (int64_t)cus * 32) blocks = (int64_t)cus * 32;
+  const bool tiled = image_tiled();
+  if (tiled) {  // padding rows and components of the fragment layout read as zeros
+    hipError_t e = hipMemsetAsync(img, 0, (size_t)((n + 31) / 32) * ((d + 15) / 16) * 1024, stream);
+    if (e != hipSuccess) {
+      set_error("image memset: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+  }
   hipLaunchKernelGGL(image_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, n, d,
-                     reinterpret_cast<_Float16*>(img), rowinfo);
+                     reinterpret_cast<_Float16*>(img), rowinfo, tiled);
   return check_launch("image_kernel");
 }
 

@@ -303,17 +303,21 @@ class Engine:
         if not t.is_contiguous() or t.data_ptr() % 16 != 0:
             return None, None
         key = id(t)
-        sig = (t.data_ptr(), tuple(t.shape), t._version)
+        # (the layout, FX_IMAGE_TILED, is read by the library at build and at search)
+        sig = (t.data_ptr(), tuple(t.shape), t._version,
+               os.environ.get("FX_IMAGE_TILED", "1") != "0")
         hit = self._images.get(key)
         if hit is not None and hit[0] == sig:
             return hit[1], hit[2]
         self._images.pop(key, None)  # a stale image: free it before building the new one
         n, d = shard.n, shard.d
-        need = n * d * 2 + n * 4
+        ib, rb = ctypes.c_size_t(0), ctypes.c_size_t(0)
+        _lib.check(_lib.load().fx_filter_image_bytes(n, d, ctypes.byref(ib), ctypes.byref(rb)))
+        need = ib.value + rb.value
         free, _ = torch.cuda.mem_get_info(self.device)
         if need + (1 << 30) > free:
             return None, None
-        img = torch.empty((n, d), dtype=torch.float16, device=self.device)
+        img = torch.empty((ib.value // 2,), dtype=torch.float16, device=self.device)
         info = torch.empty((n,), dtype=torch.float32, device=self.device)
         _lib.check(_lib.load().fx_filter_image(_ptr(t), n, d, _ptr(img), _ptr(info),
                                                self._stream()))

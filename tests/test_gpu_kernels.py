@@ -568,6 +568,32 @@ def _extreme_rows(n, d, seed):
     return xh
 
 
+def _build_image(x, n, d):
+    """fx_filter_image into buffers of fx_filter_image_bytes."""
+    import ctypes
+    ib, rb = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    _lib.check(_lib.load().fx_filter_image_bytes(n, d, ctypes.byref(ib), ctypes.byref(rb)))
+    img = torch.empty((ib.value // 2,), dtype=torch.float16, device=x.device)
+    info = torch.empty((n,), dtype=torch.float32, device=x.device)
+    _lib.check(_lib.load().fx_filter_image(x.data_ptr(), n, d, img.data_ptr(), info.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    return img, info
+
+
+def _image_rows(img, n, d):
+    """[n, d] fp16 rows of a filter image: the MFMA-fragment layout
+    [tile][k-step][lane half][row in tile][8] (the default, padding zero) or
+    row-major (FX_IMAGE_TILED=0)."""
+    h = img.cpu().numpy()
+    if os.environ.get("FX_IMAGE_TILED", "1") == "0":
+        return h.reshape(n, d)
+    t, ks = (n + 31) // 32, (d + 15) // 16
+    full = h.reshape(t, ks, 2, 32, 8).transpose(0, 3, 1, 2, 4).reshape(t * 32, ks * 16)
+    assert not full[n:].any() and not full[:, d:].any(), "image padding is not zero"
+    return full[:n, :d]
+
+
 def test_filter_image_contents(eng):
     """fx_filter_image: each component rounded to nearest-even fp16 (torch's
     own conversion, bit for bit, infinities included), rowinfo = the row's sum
@@ -576,13 +602,9 @@ def test_filter_image_contents(eng):
     n, d = 5_003, 136
     xh = _extreme_rows(n, d, 41)
     x = torch.from_numpy(xh).to(eng.device)
-    img = torch.empty((n, d), dtype=torch.float16, device=eng.device)
-    info = torch.empty((n,), dtype=torch.float32, device=eng.device)
-    _lib.check(_lib.load().fx_filter_image(x.data_ptr(), n, d, img.data_ptr(), info.data_ptr(),
-                                           torch.cuda.current_stream().cuda_stream))
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(img.cpu().numpy().view(np.uint16),
-                                  x.half().cpu().numpy().view(np.uint16))
+    img, info = _build_image(x, n, d)
+    want = x.half().cpu().numpy().view(np.uint16)
+    np.testing.assert_array_equal(_image_rows(img, n, d).view(np.uint16), want)
     got = info.cpu().numpy()
     with np.errstate(over="ignore", invalid="ignore"):
         ss = np.sum(xh.astype(np.float64) ** 2, axis=1)
@@ -610,17 +632,23 @@ def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k):
     q = O.fill_normal(nq, d, seed=44)
     q[0] *= 2.0 ** 50
     q[min(1, nq - 1)] = xh[7] if nq > 1 else q[0]
-    for v in ("FX_BATCH", "FX_BATCH_FILTER", "FX_FILTER_RING", "FENIX_AMD_FILTER_IMAGE"):
+    for v in ("FX_BATCH", "FX_BATCH_FILTER", "FX_FILTER_RING", "FENIX_AMD_FILTER_IMAGE",
+              "FX_IMAGE_TILED"):
         monkeypatch.delenv(v, raising=False)
     assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, nq, k, _lib.METRICS[metric])
     eng._images.clear()
-    id_, ir = gpu_search(eng, x, q, metric, k)
+    id_, ir = gpu_search(eng, x, q, metric, k)  # MFMA-fragment-order image (default)
     assert id(x) in eng._images  # the image path ran
+    monkeypatch.setenv("FX_IMAGE_TILED", "0")  # row-major image, register-staged kernels
+    eng._images.clear()
+    rd, rr_ = gpu_search(eng, x, q, metric, k)
+    eng._images.clear()
+    monkeypatch.delenv("FX_IMAGE_TILED")
     monkeypatch.setenv("FENIX_AMD_FILTER_IMAGE", "0")
     nd, nr = gpu_search(eng, x, q, metric, k)
     monkeypatch.setenv("FX_BATCH", "0")
     sd, sr = gpu_search(eng, x, q, metric, k)
-    for dd, rr in ((id_, ir), (nd, nr)):
+    for dd, rr in ((id_, ir), (rd, rr_), (nd, nr)):
         np.testing.assert_array_equal(rr, sr)
         np.testing.assert_array_equal(dd.view(np.uint32), sd.view(np.uint32))
 
