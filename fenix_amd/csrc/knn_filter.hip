@@ -292,6 +292,26 @@ __device__ __forceinline__ void filter_compute(f32x16 (&acc)[2][fQT], unsigned c
   }
 }
 
+// Calls f(integral_constant<int, I>) for I = 0 .. N-1 (indices stay static)
+template <int N, typename F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, F, I + 1>(static_cast<F&&>(f));
+  }
+}
+
+// static_for when STATIC, else a plain unrolled loop (the compiler's choice)
+template <bool STATIC, int N, typename F>
+__device__ __forceinline__ void unroll_for(F&& f) {
+  if constexpr (STATIC) {
+    static_for<N>(static_cast<F&&>(f));
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) f(i);
+  }
+}
+
 // Per-query constants of the pass test (once per block).  The test lb <= T
 // is linear in the product x for a fixed row, so it is precomputed as
 // x >= a * rv + b with rv the row's value (cosine: max(|x|, 1e-12); IP: |x|;
@@ -475,6 +495,139 @@ __device__ __forceinline__ void filter_epilogue(const f32x16 (&acc)[RT][QT], con
       }
       }
     }
+}
+
+// filter_epilogue with the appends staged in LDS: they go to a per-(workgroup, query) LDS segment of SEG
+// entries {lb key, ub key, row} (slot from an LDS atomic: no global atomic
+// and no global store on the tile boundary), flushed at the kernel's end
+// (filter_flush_segments); entries past SEG take a global slot as before.
+template <int METRIC, int QT, int RT, int SEG>
+__device__ __forceinline__ void filter_epilogue_seg(const f32x16 (&acc)[RT][QT], const float* rinfo,
+                                                const float* rterm, const uint32_t* flags,
+                                                const f32x4* qtab, const float2* qab,
+                                                const FilterArgs& a, int64_t q0, int64_t r0,
+                                                int rg, int qg, int h, int l32, int diag,
+                                                uint32_t* seg) {
+    constexpr int NR = 16 * RT;  // rows per lane
+    constexpr uint32_t kAll = NR == 32 ? ~0u : (1u << NR) - 1u;
+    const int lr0 = rg * 32 * RT + 4 * h;
+    const float* ri = rinfo + lr0;
+    const uint32_t grow0 = (uint32_t)(a.row_base + r0 + lr0);
+    // row j of the lane (acc register j & 15 of row tile j >> 4) sits at a
+    // compile-time offset from ri: row values are re-read from LDS where used
+    auto roff = [](int j) { return (j >> 4) * 32 + (j & 3) + 8 * ((j & 15) >> 2); };
+    const uint32_t fmask = flags[rg * 2 + h], smask = flags[16 + rg * 2 + h];
+    uint32_t pm[QT];
+#pragma unroll
+    for (int u = 0; u < QT; ++u) {
+      const float2 ab = qab[qg * QT * 32 + u * 32 + l32];
+      // fail bits: sign of RN(x - t) is set exactly when x < t (x, t finite;
+      // RN never flips a sign, x == t gives +0); bit j enters last-in at
+      // bit 0, so j runs down
+      uint32_t fail = 0u;
+#pragma unroll
+      for (int j = NR - 1; j >= 0; --j) {
+        const float t = fmaf(ab.x, ri[roff(j)], ab.y);
+        fail = __builtin_amdgcn_alignbit(fail, __float_as_uint(acc[j >> 4][u][j & 15] - t), 31);
+      }
+      pm[u] = (diag & 1) ? 0u : ((~fail | fmask) & ~smask & kAll);
+      if (q0 + qg * QT * 32 + u * 32 + l32 >= a.nq) pm[u] = 0u;
+    }
+    uint32_t any = 0u;
+#pragma unroll
+    for (int u = 0; u < QT; ++u) any |= pm[u];
+    if (__ballot(any != 0u) == 0ull) return;
+    uint32_t pos[QT];
+#pragma unroll
+    for (int u = 0; u < QT; ++u) {
+      pos[u] = 0u;
+      const int64_t gq = q0 + qg * QT * 32 + u * 32 + l32;
+      if (pm[u] != 0u) {
+        if constexpr (SEG > 0)  // LDS counter of the query (seg[0 .. fBQ))
+          pos[u] = atomicAdd(&seg[qg * QT * 32 + u * 32 + l32], (uint32_t)__popc(pm[u]));
+        else if ((diag & 32) && a.cand_ub != nullptr)  // profiling only (final phase): no atomic
+          pos[u] = (uint32_t)l32 * 64u;
+        else
+          pos[u] = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(pm[u]));
+      }
+    }
+    unroll_for<(SEG > 0), QT>([&](auto uc) {
+      const int u = uc;
+      if (__ballot(pm[u] != 0u) == 0ull) return;
+      const int qi = qg * QT * 32 + u * 32 + l32;
+      const int64_t gq = q0 + qi;
+      const f32x4 qc = qtab[qi];
+      const float qc1 = qc[0], qc0 = qc[1], qA = qc[2], qB = qc[3];
+      const bool fq = !(qA <= 3.4e38f);
+      uint32_t p = pos[u];
+      uint32_t gp = ~0u;
+      // rows in groups of 4: a group no lane of the wave appends from is
+      // skipped with one wave-uniform branch (a few appends per wave and tile)
+      unroll_for<(SEG > 0), NR / 4>([&](auto gc) {
+        const int g = gc;
+        if (__ballot(((pm[u] >> (4 * g)) & 0xfu) != 0u) == 0ull) return;
+      unroll_for<(SEG > 0), 4>([&](auto jc) {
+        const int j = 4 * g + (int)jc;
+        if (!((pm[u] >> j) & 1u)) return;
+        const float rv = ri[roff(j)];
+        const float x = acc[j >> 4][u][j & 15];
+        float lb, ub;
+        if constexpr (METRIC == 0) {
+          const float s2 = rv + qc0;
+          const float d2 = fmaf(x, qc1, s2);
+          const float e = fmaf(qA, s2, qB);
+          lb = sqrtf(fmaxf(d2 - e, 0.f));
+          ub = sqrtf(d2 + e);
+        } else if constexpr (METRIC == 1) {
+          const float e = fmaf(qA, rv, qB);
+          lb = fmaf(x, qc1, -e);
+          ub = fmaf(x, qc1, e);
+        } else {
+          const float rt = rterm[lr0 + roff(j)];
+          const float dist = fmaf(x * rt, qc1, 0.5f);
+          const float e = fmaf(qB, rt, qA);
+          lb = dist - e;
+          ub = dist + e;
+        }
+        if (fq || rv != rv) {  // forced: below / above every key
+          lb = -__builtin_inff();
+          ub = __builtin_nanf("");
+        }
+        if constexpr (SEG > 0) {
+          const uint32_t grow = grow0 + (uint32_t)roff(j);
+          if (p < (uint32_t)SEG) {
+            uint32_t* e = seg + fBQ + 3 * (qi * SEG + p);
+            e[0] = order_key(lb);
+            e[1] = order_key(ub);
+            e[2] = grow;
+          } else {  // rare: past the segment, global slots for the lane's remaining passes
+            if (gp == ~0u) gp = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(pm[u] >> j));
+            if (gp < (uint32_t)a.cap) {
+              const size_t slot = (size_t)gq * a.cap + gp;
+              if (a.cand_ub != nullptr) {
+                a.cand[slot] = make_comp(lb, grow);
+                a.cand_ub[slot] = make_comp(ub, grow);
+              } else {
+                a.cand[slot] = make_comp(ub, grow);
+              }
+            }
+            ++gp;
+          }
+        } else
+        if (p < (uint32_t)a.cap && !((diag & 64) && a.cand_ub != nullptr)) {  // (64: profiling)
+          const uint32_t grow = grow0 + (uint32_t)roff(j);
+          const size_t slot = (size_t)gq * a.cap + p;
+          if (a.cand_ub != nullptr) {
+            a.cand[slot] = make_comp(lb, grow);
+            a.cand_ub[slot] = make_comp(ub, grow);
+          } else {
+            a.cand[slot] = make_comp(ub, grow);
+          }
+        }
+        ++p;
+      });
+      });
+    });
 }
 
 // The tile loop of filter_kernel.  SF (store first): the wave stores chunk
@@ -688,7 +841,43 @@ __device__ __forceinline__ void filter_tiles(const FilterArgs& a, unsigned char*
   }
 }
 
+// Write a workgroup's LDS append segments (filter_epilogue_seg) to the
+// candidate buffer: one global atomic per query reserves the slots.  seg =
+// [fBQ counters][fBQ x SEG entries {lb key, ub key, row}]; called by every
+// thread after the last tile (ends with the counters reused as bases).
+template <int SEG>
+__device__ __forceinline__ void filter_flush_segments(uint32_t* seg, uint32_t* base,
+                                                      const FilterArgs& a, int64_t q0, int tid) {
+  __syncthreads();
+  for (int q = tid; q < fBQ; q += fThreads) {
+    const uint32_t n = seg[q] < (uint32_t)SEG ? seg[q] : (uint32_t)SEG;
+    seg[q] = n;
+    base[q] = n != 0u && q0 + q < a.nq ? atomicAdd(&a.count[(q0 + q) * kCountStride], n) : 0u;
+  }
+  __syncthreads();
+  for (int i = tid; i < fBQ * SEG; i += fThreads) {
+    const int q = i / SEG, j = i % SEG;
+    if ((uint32_t)j >= seg[q]) continue;
+    const uint32_t p = base[q] + (uint32_t)j;
+    if (p >= (uint32_t)a.cap) continue;
+    const uint32_t* e = seg + fBQ + 3 * i;
+    const size_t slot = (size_t)(q0 + q) * a.cap + p;
+    if (a.cand_ub != nullptr) {
+      a.cand[slot] = ((uint64_t)e[0] << 32) | e[2];
+      a.cand_ub[slot] = ((uint64_t)e[1] << 32) | e[2];
+    } else {
+      a.cand[slot] = ((uint64_t)e[1] << 32) | e[2];
+    }
+  }
+}
+
 // ------------------------------------------------------ tiled filter image
+#ifndef FX_I2_SEG
+#define FX_I2_SEG 32  // LDS append segment per query (0: a global atomic per lane and query)
+#endif
+#ifndef FX_I2_STAGES
+#define FX_I2_STAGES 2  // row chunks in flight per wave (filter_img2_kernel)
+#endif
 //
 // The fp16 image of an f32 corpus in MFMA fragment order (FX_IMAGE_TILED,
 // default on), [ceil(n / 32) row tiles][ceil(d / 16) k-steps][64 lanes][8
@@ -704,6 +893,10 @@ struct Img2Shared {
   uint32_t rflags[2][kRowFlagWords];
   f32x4 qtab[fBQ];
   float2 qab[fBQ];
+#if FX_I2_SEG > 0
+  uint32_t seg[fBQ + 3 * fBQ * FX_I2_SEG];  // counters, then entries (filter_epilogue_seg)
+  uint32_t segbase[fBQ];
+#endif
 };
 constexpr int kI2QT = fBQ / 32;  // query tiles per wave (every query)
 constexpr int kI2KS = fBK / 16;  // k-steps per chunk
@@ -726,6 +919,9 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
   constexpr int diag = 0;
 #endif
   filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
+#if FX_I2_SEG > 0
+  for (int q = tid; q < fBQ; q += fThreads) sh->seg[q] = 0u;  // (ordered by the tile barriers)
+#endif
 
   FilterAddr ad;  // the query tile (as filter_tiles)
   {
@@ -801,13 +997,45 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
         }
       }
     };
-    XA xa0, xa1;
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
     FilterPreQ pq;
+#if FX_I2_STAGES != 2
+    {  // S row chunks in flight: step c multiplies xa[c % S] and reloads it
+       // with chunk c + S; U steps per loop trip keep every index static
+      constexpr int S = FX_I2_STAGES, U = S % 2 ? 2 * S : S;
+      XA xa[S];
+      filter_load_q(pq, ad, o, 0, diag);
+#pragma unroll
+      for (int s = 0; s < S; ++s) load_x(xa[s], s);
+      store_q(pq, B0{});
+      filter_load_q(pq, ad, o, 1, diag);
+      __syncthreads();
+      auto stepS = [&](int c, XA& x, auto buf) {
+        constexpr int B = decltype(buf)::value;
+        compute(x, buf);
+        store_q(pq, std::integral_constant<int, B ^ 1>{});  // (past the end: zeros)
+        filter_load_q(pq, ad, o, c + 2, diag);
+        load_x(x, c + S);
+        __syncthreads();
+      };
+      int c = 0;
+      for (; c + U <= nch; c += U) {
+        static_for<U>([&](auto j) {
+          constexpr int J = decltype(j)::value;
+          stepS(c + J, xa[J % S], std::integral_constant<int, J & 1>{});
+        });
+      }
+      static_for<U - 1>([&](auto j) {  // the tail: fewer than U chunks
+        constexpr int J = decltype(j)::value;
+        if (c + J < nch) stepS(c + J, xa[J % S], std::integral_constant<int, J & 1>{});
+      });
+    }
+#else
+    XA xa0, xa1;
     filter_load_q(pq, ad, o, 0, diag);
     load_x(xa0, 0);
     load_x(xa1, 1);
-    using B0 = std::integral_constant<int, 0>;
-    using B1 = std::integral_constant<int, 1>;
     store_q(pq, B0{});
     filter_load_q(pq, ad, o, 1, diag);
     __syncthreads();
@@ -831,6 +1059,7 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
     __syncthreads();
     compute(xa0, B0{});
     if (two) compute(xa1, B1{});
+#endif
 
     if (tid < fBM) {  // one thread per row: bound factor, flags
       const int lr = tid;
@@ -854,9 +1083,174 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
       if (acc[0][0][0] == 1.2345f) a.count[0] = 7;
       continue;
     }
+#if FX_I2_SEG > 0
+    filter_epilogue_seg<METRIC, kI2QT, 1, FX_I2_SEG>(acc, sh->rinfo, sh->rterm, sh->rflags[par],
+                                                 sh->qtab, sh->qab, a, q0, r0, wid, 0, h, l32,
+                                                 diag, sh->seg);
+#else
     filter_epilogue<METRIC, kI2QT, 1>(acc, sh->rinfo, sh->rterm, sh->rflags[par], sh->qtab,
                                       sh->qab, a, q0, r0, wid, 0, h, l32, diag);
+#endif
   }
+#if FX_I2_SEG > 0
+  filter_flush_segments<FX_I2_SEG>(sh->seg, sh->segbase, a, q0, tid);
+#endif
+}
+
+// The tiled-image filter with one continuous stream across tiles: the last
+// FX_I2_STAGES steps of a tile load the NEXT tile's first row chunks (and the
+// query chunks wrap round to 0 and 1), so the stream stays busy through the
+// bound factors and the epilogue, and a tile starts with its operands in
+// flight.  Needs chunks per row % U == 0 (launch_img2 checks); the rows'
+// image sums and mask words are loaded at the tile start, before the stream.
+#ifndef FX_I2_XPF
+#define FX_I2_XPF 0
+#endif
+template <int METRIC>
+__global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(FilterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Img2Shared* sh = reinterpret_cast<Img2Shared*>(smem);
+  constexpr int S = FX_I2_STAGES < 2 ? 2 : FX_I2_STAGES, U = S % 2 ? 2 * S : S;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, l32 = lane & 31;
+  const int64_t q0 = (int64_t)blockIdx.y * fBQ;
+  const int nch = (a.d + fBK - 1) / fBK;
+  const int ksteps = (a.d + 15) / 16;
+  const int64_t ntile32 = (a.n + 31) / 32;
+  filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
+  int64_t ti = blockIdx.x;
+  if (ti >= a.num_tiles) return;
+
+  FilterAddr ad;  // the query tile (as filter_img2_kernel)
+  {
+    const uint16_t* qb = a.Qh + q0 * 32;
+    const uint64_t qp = reinterpret_cast<uint64_t>(qb);
+    const uint32_t qlo = __builtin_amdgcn_readfirstlane((uint32_t)qp);
+    const uint32_t qhi = __builtin_amdgcn_readfirstlane((uint32_t)(qp >> 32));
+    const int qnb = __builtin_amdgcn_readfirstlane(
+        (int)(((int64_t)(a.dq / 32 - 1) * a.qstride + fBQ) * 64));
+    ad.qr = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)qhi << 32) | qlo), 0, qnb, 0x00020000);
+    ad.d = a.d;
+    ad.xs = 0;
+    ad.qs = (uint32_t)(fThreads / fQC) * 64u;
+    ad.qb = (uint32_t)a.qstride * 64u;
+    ad.dq = a.dq;
+  }
+  FilterOff o = {};
+  {
+    const unsigned t = opaque(tid);
+    o.qg = (t / fQC) * 64 + (t % fQC) % 4 * 16 + (t % fQC) / 4 * ad.qb;
+  }
+  const uint32_t qw = ((tid / fQC) * fLds + (tid % fQC) * 8) * 2;
+  const uint32_t qr = (l32 * fLds + 8 * h) * 2;
+  auto store_q = [&](const FilterPreQ& pq, auto buf) {
+    constexpr int B = decltype(buf)::value;
+#pragma unroll
+    for (int i = 0; i < fQP; ++i)
+      lds_at<i32x4>(smem, B * kQB + qw + i * (fThreads / fQC) * fLds * 2) = pq.q[i];
+  };
+  // this wave's 32-row tile of tile t: base address and size (0 past the end)
+  auto tile_base = [&](int64_t t, uint64_t& base, int& nb) {
+    const int64_t t32 = (a.tile_start + t * a.tile_stride) * (fBM / 32) + wid;
+    const bool live = t < a.num_tiles && t32 < ntile32;
+    base = reinterpret_cast<uint64_t>(a.X) + (uint64_t)(live ? t32 : 0) * ksteps * 1024;
+    nb = live ? ksteps * 1024 : 0;
+  };
+  const uint32_t xl = (uint32_t)opaque(lane) * 16u;
+  typedef f16x8 XA[kI2KS];
+  auto load_x = [&](XA& xa, uint64_t base, int nb, int c) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, __builtin_amdgcn_readfirstlane(nb),
+        0x00020000);
+#pragma unroll
+    for (int s = 0; s < kI2KS; ++s) {
+      const int ks = c * kI2KS + s;
+      const uint32_t off = ks < ksteps ? xl : 0x7fff0000u;
+      xa[s] = __builtin_bit_cast(
+          f16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, ks * 1024, 2 /* nt */));
+    }
+  };
+  using B0 = std::integral_constant<int, 0>;
+  XA xa[S];
+  FilterPreQ pq;
+  uint64_t cur;
+  int ncur;
+  tile_base(ti, cur, ncur);
+  filter_load_q(pq, ad, o, 0, 0);
+#pragma unroll
+  for (int s = 0; s < S; ++s) load_x(xa[s], cur, ncur, s);
+  store_q(pq, B0{});
+  filter_load_q(pq, ad, o, 1, 0);
+  __syncthreads();
+
+  int par = 0;
+  for (; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
+    const int64_t r0 = (a.tile_start + ti * a.tile_stride) * fBM;
+    uint64_t nxt;
+    int nnxt;
+    tile_base(ti + gridDim.x, nxt, nnxt);
+    // this thread's row: image sum and mask word, before the stream's loads
+    float rsum = 0.f;
+    uint32_t mword = ~0u;
+    const int64_t row = r0 + tid;
+    if (tid < fBM && row < a.n) {
+      rsum = a.rowinfo[row];
+      if (a.mask != nullptr) mword = a.mask[row >> 5];
+    }
+    if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;
+    f32x16 acc[1][kI2QT];
+#pragma unroll
+    for (int u = 0; u < kI2QT; ++u) acc[0][u] = f32x16(0.f);
+    auto step = [&](int c, XA& x, auto buf) {
+      constexpr int B = decltype(buf)::value;
+#pragma unroll
+      for (int s = 0; s < kI2KS; ++s) {
+#pragma unroll
+        for (int u = 0; u < kI2QT; ++u) {
+          const f16x8 bv = lds_at<f16x8>(smem, B * kQB + qr + (u * 32 * fLds + 16 * s) * 2);
+          acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(x[s], bv, acc[0][u], 0, 0, 0);
+        }
+      }
+      store_q(pq, std::integral_constant<int, B ^ 1>{});
+      const int cq = c + 2 < nch ? c + 2 : c + 2 - nch;  // query chunks wrap round
+      filter_load_q(pq, ad, o, cq, 0);
+      const bool nx = c + S >= nch;  // wave-uniform selects, no branch
+      load_x(x, nx ? nxt : cur, nx ? nnxt : ncur, nx ? c + S - nch : c + S);
+      __syncthreads();
+    };
+    for (int c = 0; c < nch; c += U) {
+      static_for<U>([&](auto j) {
+        constexpr int J = decltype(j)::value;
+        step(c + J, xa[J % S], std::integral_constant<int, J & 1>{});
+      });
+    }
+    cur = nxt;
+    ncur = nnxt;
+
+    if (tid < fBM) {  // one thread per row: bound factor, flags
+      bool ok = row < a.n && ((mword >> (row & 31)) & 1u);
+      const float s = ok ? rsum : 0.f;
+      float rv;
+      if constexpr (METRIC == 0) {
+        rv = s;
+      } else if constexpr (METRIC == 1) {
+        rv = sqrtf(s);
+      } else {
+        rv = fmaxf(sqrtf(s), 1e-12f);
+      }
+      if (!(s <= 3.4e38f)) rv = __builtin_nanf("");
+      filter_note_row<METRIC, 1>(sh->rinfo, sh->rterm, sh->rflags[par], tid, rv, ok);
+    }
+    __syncthreads();
+    filter_epilogue<METRIC, kI2QT, 1>(acc, sh->rinfo, sh->rterm, sh->rflags[par], sh->qtab,
+                                      sh->qab, a, q0, r0, wid, 0, h, l32, 0);
+  }
+  // the stream's last loads (empty descriptors past the end) land before exit
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 static int launch_img2(const FilterArgs& a, int metric, hipStream_t stream) {
@@ -864,6 +1258,14 @@ static int launch_img2(const FilterArgs& a, int metric, hipStream_t stream) {
   const void* fn = metric == FX_METRIC_COS ? (const void*)filter_img2_kernel<2>
                    : metric == FX_METRIC_IP ? (const void*)filter_img2_kernel<1>
                                             : (const void*)filter_img2_kernel<0>;
+  {
+    constexpr int S = FX_I2_STAGES < 2 ? 2 : FX_I2_STAGES, U = S % 2 ? 2 * S : S;
+    const int nch = (a.d + fBK - 1) / fBK;
+    if (FX_I2_XPF && nch % U == 0 && a.diag == 0)
+      fn = metric == FX_METRIC_COS ? (const void*)filter_img3_kernel<2>
+           : metric == FX_METRIC_IP ? (const void*)filter_img3_kernel<1>
+                                    : (const void*)filter_img3_kernel<0>;
+  }
   if (int rc = allow_lds(fn)) return rc;
   int cus = 0;
   int rc = device_cus(&cus);
