@@ -872,8 +872,9 @@ __device__ __forceinline__ void filter_flush_segments(uint32_t* seg, uint32_t* b
 }
 
 // ------------------------------------------------------ tiled filter image
-#ifndef FX_I2_SEG
-#define FX_I2_SEG 32  // LDS append segment per query (0: a global atomic per lane and query)
+#ifndef FX_I2_SEG  // LDS append segment per query (0: a global atomic per lane and query);
+                   // the 256-query, 64-wide-K compilation has room for 16 (Img2Shared)
+#define FX_I2_SEG (FX_FILTER_BQ >= 256 && FX_FILTER_BK >= 64 ? 16 : 32)
 #endif
 #ifndef FX_I2_STAGES
 #define FX_I2_STAGES 2  // row chunks in flight per wave (filter_img2_kernel)
@@ -898,6 +899,7 @@ struct Img2Shared {
   uint32_t segbase[fBQ];
 #endif
 };
+static_assert(sizeof(Img2Shared) <= 160 * 1024, "filter_img2_kernel: LDS over 160 KB");
 constexpr int kI2QT = fBQ / 32;  // query tiles per wave (every query)
 constexpr int kI2KS = fBK / 16;  // k-steps per chunk
 static_assert(fWaves * 32 == fBM, "tiled image: one 32-row tile per wave");
@@ -988,6 +990,10 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
     for (int u = 0; u < kI2QT; ++u) acc[0][u] = f32x16(0.f);
     auto compute = [&](const XA& xa, auto buf) {
       constexpr int B = decltype(buf)::value;
+      if (diag & 4) {  // (diagnostics: no MFMA; the row loads stay live)
+        if (xa[0][0] == (_Float16)1.2345f && xa[kI2KS - 1][7] == (_Float16)2.f) a.count[0] = 7;
+        return;
+      }
 #pragma unroll
       for (int s = 0; s < kI2KS; ++s) {
 #pragma unroll
