@@ -873,8 +873,9 @@ __device__ __forceinline__ void filter_flush_segments(uint32_t* seg, uint32_t* b
 
 // ------------------------------------------------------ tiled filter image
 #ifndef FX_I2_SEG  // LDS append segment per query (0: a global atomic per lane and query);
-                   // the 256-query, 64-wide-K compilation has room for 16 (Img2Shared)
-#define FX_I2_SEG (FX_FILTER_BQ >= 256 && FX_FILTER_BK >= 64 ? 16 : 32)
+                   // 64-query tiles only: 16 entries in the 256-query build (the most
+                   // its LDS holds) measured 3.5 % slower
+#define FX_I2_SEG (FX_FILTER_BQ >= 256 ? 0 : 32)
 #endif
 #ifndef FX_I2_STAGES
 #define FX_I2_STAGES 2  // row chunks in flight per wave (filter_img2_kernel)
