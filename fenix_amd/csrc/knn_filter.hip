@@ -1846,24 +1846,16 @@ typedef float img_f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 img_f16x4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256) image_kernel(const float* __restrict__ X, int64_t n, int d,
                                                     _Float16* __restrict__ img,
-                                                    float* __restrict__ rowinfo, bool tiled) {
+                                                    float* __restrict__ rowinfo) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
-  const int64_t ksteps = (d + 15) / 16;
   for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += nw) {
     const img_f32x4* xr = reinterpret_cast<const img_f32x4*>(X + r * d);
     img_f16x4* ir = reinterpret_cast<img_f16x4*>(img + r * d);
     float s = 0.f, m = 0.f;
     for (int i = lane; i < d / 4; i += 64) {
       const img_f32x4 v = __builtin_nontemporal_load(xr + i);
-      if (tiled) {  // components 4i..4i+3 of row r at their MFMA-fragment position
-        const int k = 4 * i;
-        const int64_t at =
-            (((r >> 5) * ksteps + (k >> 4)) * 64 + (r & 31) + 32 * ((k & 15) >> 3)) * 8 + (k & 7);
-        *reinterpret_cast<img_f16x4*>(img + at) = __builtin_convertvector(v, img_f16x4);
-      } else {
-        ir[i] = __builtin_convertvector(v, img_f16x4);
-      }
+      ir[i] = __builtin_convertvector(v, img_f16x4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         s = fmaf(v[e], v[e], s);
@@ -1879,24 +1871,72 @@ __global__ void __launch_bounds__(256) image_kernel(const float* __restrict__ X,
   }
 }
 
+// The image in MFMA fragment order (FX_IMAGE_TILED): one wave per 32-row
+// tile, grid-stride.  Each k-step, lane l reads components 16 s + 8 (l / 32)
+// .. + 7 of row 32 t + l % 32 (two 16-B loads; the other half of each line is
+// read by the next k-step, from L2) and the wave writes the k-step's KB of
+// the image as one contiguous store.  Padding rows and components are written
+// as zeros (no memset).  d % 8 == 0 (fx_filter_image checks).
+typedef _Float16 img_f16x8 __attribute__((ext_vector_type(8)));
+__global__ void __launch_bounds__(256) image_tiled_kernel(const float* __restrict__ X, int64_t n,
+                                                          int d, _Float16* __restrict__ img,
+                                                          float* __restrict__ rowinfo) {
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int64_t nt = (n + 31) / 32;
+  const int ksteps = (d + 15) / 16;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < nt; t += nw) {
+    const int64_t r = t * 32 + (lane & 31);
+    const bool live = r < n;
+    const float* xr = X + (live ? r : 0) * (int64_t)d;
+    img_f16x8* out = reinterpret_cast<img_f16x8*>(img) + t * ksteps * 64 + lane;
+    float s = 0.f, m = 0.f;
+#pragma unroll 4
+    for (int ks = 0; ks < ksteps; ++ks) {
+      // loads without a branch (several k-steps in flight): padding reads a
+      // valid address and is zeroed after
+      const int k0 = 16 * ks + 8 * h;
+      const bool ok = live && k0 < d;
+      const float* p = xr + (k0 < d ? k0 : 0);
+      img_f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const img_f32x4*>(p));
+      img_f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const img_f32x4*>(p + 4));
+      if (!ok) {
+        a = img_f32x4(0.f);
+        b = img_f32x4(0.f);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s = fmaf(a[e], a[e], s);
+        s = fmaf(b[e], b[e], s);
+        m = fmaxf(m, fmaxf(fabsf(a[e]), fabsf(b[e])));
+      }
+      const img_f16x4 ca = __builtin_convertvector(a, img_f16x4);
+      const img_f16x4 cb = __builtin_convertvector(b, img_f16x4);
+      out[ks * 64] = __builtin_shufflevector(ca, cb, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    s += __shfl_xor(s, 32);
+    m = fmaxf(m, __shfl_xor(m, 32));
+    if (h == 0 && live) rowinfo[r] = (s <= 3.4e38f && m < 65520.f) ? s : __builtin_nanf("");
+  }
+}
+
 int launch_image(const float* X, int64_t n, int d, void* img, float* rowinfo,
                  hipStream_t stream) {
   if (n <= 0) return FX_OK;
   int cus = 0;
   int rc = device_cus(&cus);
   if (rc) return rc;
+  if (image_tiled()) {
+    int64_t blocks = ((n + 31) / 32 + 3) / 4;
+    if (blocks > (int64_t)cus * 8) blocks = (int64_t)cus * 8;
+    hipLaunchKernelGGL(image_tiled_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, n, d,
+                       reinterpret_cast<_Float16*>(img), rowinfo);
+    return check_launch("image_tiled_kernel");
+  }
   int64_t blocks = (n + 3) / 4;
   if (blocks > (int64_t)cus * 32) blocks = (int64_t)cus * 32;
-  const bool tiled = image_tiled();
-  if (tiled) {  // padding rows and components of the fragment layout read as zeros
-    hipError_t e = hipMemsetAsync(img, 0, (size_t)((n + 31) / 32) * ((d + 15) / 16) * 1024, stream);
-    if (e != hipSuccess) {
-      set_error("image memset: %s", hipGetErrorString(e));
-      return FX_EHIP;
-    }
-  }
   hipLaunchKernelGGL(image_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, n, d,
-                     reinterpret_cast<_Float16*>(img), rowinfo, tiled);
+                     reinterpret_cast<_Float16*>(img), rowinfo);
   return check_launch("image_kernel");
 }
 
