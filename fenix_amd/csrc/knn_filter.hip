@@ -872,13 +872,14 @@ __device__ __forceinline__ void filter_flush_segments(uint32_t* seg, uint32_t* b
 }
 
 // ------------------------------------------------------ tiled filter image
+#ifndef FX_FILTER_IMG2  // compiled into the 64-query and the 32-wide-K 256-query builds
+                        // (the 64-wide-K h256 build measured 7 % slower on it)
+#define FX_FILTER_IMG2 (FX_FILTER_BQ == 64 || FX_FILTER_BK == 32)
+#endif
 #ifndef FX_I2_SEG  // LDS append segment per query (0: a global atomic per lane and query);
                    // 64-query tiles only: 16 entries in the 256-query build (the most
                    // its LDS holds) measured 3.5 % slower
 #define FX_I2_SEG (FX_FILTER_BQ >= 256 ? 0 : 32)
-#endif
-#ifndef FX_I2_STAGES
-#define FX_I2_STAGES 2  // row chunks in flight per wave (filter_img2_kernel)
 #endif
 //
 // The fp16 image of an f32 corpus in MFMA fragment order (FX_IMAGE_TILED,
@@ -1007,38 +1008,6 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
     FilterPreQ pq;
-#if FX_I2_STAGES != 2
-    {  // S row chunks in flight: step c multiplies xa[c % S] and reloads it
-       // with chunk c + S; U steps per loop trip keep every index static
-      constexpr int S = FX_I2_STAGES, U = S % 2 ? 2 * S : S;
-      XA xa[S];
-      filter_load_q(pq, ad, o, 0, diag);
-#pragma unroll
-      for (int s = 0; s < S; ++s) load_x(xa[s], s);
-      store_q(pq, B0{});
-      filter_load_q(pq, ad, o, 1, diag);
-      __syncthreads();
-      auto stepS = [&](int c, XA& x, auto buf) {
-        constexpr int B = decltype(buf)::value;
-        compute(x, buf);
-        store_q(pq, std::integral_constant<int, B ^ 1>{});  // (past the end: zeros)
-        filter_load_q(pq, ad, o, c + 2, diag);
-        load_x(x, c + S);
-        __syncthreads();
-      };
-      int c = 0;
-      for (; c + U <= nch; c += U) {
-        static_for<U>([&](auto j) {
-          constexpr int J = decltype(j)::value;
-          stepS(c + J, xa[J % S], std::integral_constant<int, J & 1>{});
-        });
-      }
-      static_for<U - 1>([&](auto j) {  // the tail: fewer than U chunks
-        constexpr int J = decltype(j)::value;
-        if (c + J < nch) stepS(c + J, xa[J % S], std::integral_constant<int, J & 1>{});
-      });
-    }
-#else
     XA xa0, xa1;
     filter_load_q(pq, ad, o, 0, diag);
     load_x(xa0, 0);
@@ -1066,7 +1035,6 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
     __syncthreads();
     compute(xa0, B0{});
     if (two) compute(xa1, B1{});
-#endif
 
     if (tid < fBM) {  // one thread per row: bound factor, flags
       const int lr = tid;
@@ -1104,175 +1072,12 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
 #endif
 }
 
-// The tiled-image filter with one continuous stream across tiles: the last
-// FX_I2_STAGES steps of a tile load the NEXT tile's first row chunks (and the
-// query chunks wrap round to 0 and 1), so the stream stays busy through the
-// bound factors and the epilogue, and a tile starts with its operands in
-// flight.  Needs chunks per row % U == 0 (launch_img2 checks); the rows'
-// image sums and mask words are loaded at the tile start, before the stream.
-#ifndef FX_I2_XPF
-#define FX_I2_XPF 0
-#endif
-template <int METRIC>
-__global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(FilterArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  Img2Shared* sh = reinterpret_cast<Img2Shared*>(smem);
-  constexpr int S = FX_I2_STAGES < 2 ? 2 : FX_I2_STAGES, U = S % 2 ? 2 * S : S;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, l32 = lane & 31;
-  const int64_t q0 = (int64_t)blockIdx.y * fBQ;
-  const int nch = (a.d + fBK - 1) / fBK;
-  const int ksteps = (a.d + 15) / 16;
-  const int64_t ntile32 = (a.n + 31) / 32;
-  filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
-  int64_t ti = blockIdx.x;
-  if (ti >= a.num_tiles) return;
-
-  FilterAddr ad;  // the query tile (as filter_img2_kernel)
-  {
-    const uint16_t* qb = a.Qh + q0 * 32;
-    const uint64_t qp = reinterpret_cast<uint64_t>(qb);
-    const uint32_t qlo = __builtin_amdgcn_readfirstlane((uint32_t)qp);
-    const uint32_t qhi = __builtin_amdgcn_readfirstlane((uint32_t)(qp >> 32));
-    const int qnb = __builtin_amdgcn_readfirstlane(
-        (int)(((int64_t)(a.dq / 32 - 1) * a.qstride + fBQ) * 64));
-    ad.qr = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(((uint64_t)qhi << 32) | qlo), 0, qnb, 0x00020000);
-    ad.d = a.d;
-    ad.xs = 0;
-    ad.qs = (uint32_t)(fThreads / fQC) * 64u;
-    ad.qb = (uint32_t)a.qstride * 64u;
-    ad.dq = a.dq;
-  }
-  FilterOff o = {};
-  {
-    const unsigned t = opaque(tid);
-    o.qg = (t / fQC) * 64 + (t % fQC) % 4 * 16 + (t % fQC) / 4 * ad.qb;
-  }
-  const uint32_t qw = ((tid / fQC) * fLds + (tid % fQC) * 8) * 2;
-  const uint32_t qr = (l32 * fLds + 8 * h) * 2;
-  auto store_q = [&](const FilterPreQ& pq, auto buf) {
-    constexpr int B = decltype(buf)::value;
-#pragma unroll
-    for (int i = 0; i < fQP; ++i)
-      lds_at<i32x4>(smem, B * kQB + qw + i * (fThreads / fQC) * fLds * 2) = pq.q[i];
-  };
-  // this wave's 32-row tile of tile t: base address and size (0 past the end)
-  auto tile_base = [&](int64_t t, uint64_t& base, int& nb) {
-    const int64_t t32 = (a.tile_start + t * a.tile_stride) * (fBM / 32) + wid;
-    const bool live = t < a.num_tiles && t32 < ntile32;
-    base = reinterpret_cast<uint64_t>(a.X) + (uint64_t)(live ? t32 : 0) * ksteps * 1024;
-    nb = live ? ksteps * 1024 : 0;
-  };
-  const uint32_t xl = (uint32_t)opaque(lane) * 16u;
-  typedef f16x8 XA[kI2KS];
-  auto load_x = [&](XA& xa, uint64_t base, int nb, int c) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, __builtin_amdgcn_readfirstlane(nb),
-        0x00020000);
-#pragma unroll
-    for (int s = 0; s < kI2KS; ++s) {
-      const int ks = c * kI2KS + s;
-      const uint32_t off = ks < ksteps ? xl : 0x7fff0000u;
-      xa[s] = __builtin_bit_cast(
-          f16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, ks * 1024, 2 /* nt */));
-    }
-  };
-  using B0 = std::integral_constant<int, 0>;
-  XA xa[S];
-  FilterPreQ pq;
-  uint64_t cur;
-  int ncur;
-  tile_base(ti, cur, ncur);
-  filter_load_q(pq, ad, o, 0, 0);
-#pragma unroll
-  for (int s = 0; s < S; ++s) load_x(xa[s], cur, ncur, s);
-  store_q(pq, B0{});
-  filter_load_q(pq, ad, o, 1, 0);
-  __syncthreads();
-
-  int par = 0;
-  for (; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
-    const int64_t r0 = (a.tile_start + ti * a.tile_stride) * fBM;
-    uint64_t nxt;
-    int nnxt;
-    tile_base(ti + gridDim.x, nxt, nnxt);
-    // this thread's row: image sum and mask word, before the stream's loads
-    float rsum = 0.f;
-    uint32_t mword = ~0u;
-    const int64_t row = r0 + tid;
-    if (tid < fBM && row < a.n) {
-      rsum = a.rowinfo[row];
-      if (a.mask != nullptr) mword = a.mask[row >> 5];
-    }
-    if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;
-    f32x16 acc[1][kI2QT];
-#pragma unroll
-    for (int u = 0; u < kI2QT; ++u) acc[0][u] = f32x16(0.f);
-    auto step = [&](int c, XA& x, auto buf) {
-      constexpr int B = decltype(buf)::value;
-#pragma unroll
-      for (int s = 0; s < kI2KS; ++s) {
-#pragma unroll
-        for (int u = 0; u < kI2QT; ++u) {
-          const f16x8 bv = lds_at<f16x8>(smem, B * kQB + qr + (u * 32 * fLds + 16 * s) * 2);
-          acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(x[s], bv, acc[0][u], 0, 0, 0);
-        }
-      }
-      store_q(pq, std::integral_constant<int, B ^ 1>{});
-      const int cq = c + 2 < nch ? c + 2 : c + 2 - nch;  // query chunks wrap round
-      filter_load_q(pq, ad, o, cq, 0);
-      const bool nx = c + S >= nch;  // wave-uniform selects, no branch
-      load_x(x, nx ? nxt : cur, nx ? nnxt : ncur, nx ? c + S - nch : c + S);
-      __syncthreads();
-    };
-    for (int c = 0; c < nch; c += U) {
-      static_for<U>([&](auto j) {
-        constexpr int J = decltype(j)::value;
-        step(c + J, xa[J % S], std::integral_constant<int, J & 1>{});
-      });
-    }
-    cur = nxt;
-    ncur = nnxt;
-
-    if (tid < fBM) {  // one thread per row: bound factor, flags
-      bool ok = row < a.n && ((mword >> (row & 31)) & 1u);
-      const float s = ok ? rsum : 0.f;
-      float rv;
-      if constexpr (METRIC == 0) {
-        rv = s;
-      } else if constexpr (METRIC == 1) {
-        rv = sqrtf(s);
-      } else {
-        rv = fmaxf(sqrtf(s), 1e-12f);
-      }
-      if (!(s <= 3.4e38f)) rv = __builtin_nanf("");
-      filter_note_row<METRIC, 1>(sh->rinfo, sh->rterm, sh->rflags[par], tid, rv, ok);
-    }
-    __syncthreads();
-    filter_epilogue<METRIC, kI2QT, 1>(acc, sh->rinfo, sh->rterm, sh->rflags[par], sh->qtab,
-                                      sh->qab, a, q0, r0, wid, 0, h, l32, 0);
-  }
-  // the stream's last loads (empty descriptors past the end) land before exit
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
+#if FX_FILTER_IMG2
 static int launch_img2(const FilterArgs& a, int metric, hipStream_t stream) {
   const size_t smem = sizeof(Img2Shared);
   const void* fn = metric == FX_METRIC_COS ? (const void*)filter_img2_kernel<2>
                    : metric == FX_METRIC_IP ? (const void*)filter_img2_kernel<1>
                                             : (const void*)filter_img2_kernel<0>;
-  {
-    constexpr int S = FX_I2_STAGES < 2 ? 2 : FX_I2_STAGES, U = S % 2 ? 2 * S : S;
-    const int nch = (a.d + fBK - 1) / fBK;
-    if (FX_I2_XPF && nch % U == 0 && a.diag == 0)
-      fn = metric == FX_METRIC_COS ? (const void*)filter_img3_kernel<2>
-           : metric == FX_METRIC_IP ? (const void*)filter_img3_kernel<1>
-                                    : (const void*)filter_img3_kernel<0>;
-  }
   if (int rc = allow_lds(fn)) return rc;
   int cus = 0;
   int rc = device_cus(&cus);
@@ -1300,6 +1105,7 @@ static int launch_img2(const FilterArgs& a, int metric, hipStream_t stream) {
   }
   return check_launch("filter_img2_kernel");
 }
+#endif  // FX_FILTER_IMG2
 
 #ifndef FX_FILTER_SPLIT  // measured slower (6.48 vs 6.35 ms for configs[2], same box)
 #define FX_FILTER_SPLIT 0
@@ -1648,7 +1454,7 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.num_tiles <= 0) return FX_OK;
   const bool f16 = a.dtype == FX_DTYPE_F16;
   if (a.rowinfo != nullptr && image_tiled()) {  // the image in MFMA fragment order
-#if FX_FILTER_ROWS & 2
+#if FX_FILTER_IMG2
     return launch_img2(a, metric, stream);
 #else
     set_error("filter: the tiled image is not compiled into this variant");
@@ -1749,6 +1555,9 @@ bool filter_ring() {
 // Batches of <= 64 queries take the 64-query tiles (their Qh is padded to 64)
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.nq <= 64) return q64::launch(a, metric, stream);
+  // tiled images: K chunks of 32 (5.07-5.10 vs 5.48-5.49 ms for configs[2]
+  // in the 64-wide h256 build, profiles/r02_filter_img_bk32.log)
+  if (a.rowinfo != nullptr && image_tiled()) return q256::launch(a, metric, stream);
   if (a.dtype == FX_DTYPE_F16 && !filter_ring()) return h256::launch(a, metric, stream);
   return q256::launch(a, metric, stream);
 }
