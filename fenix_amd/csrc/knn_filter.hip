@@ -53,7 +53,8 @@
 
 // This file is compiled twice: as itself (256-query tiles, namespace
 // fx::q256, plus the shared entry points) and through knn_filter_q64.hip
-// (FX_FILTER_VARIANT: 64-query tiles, namespace fx::q64) for small batches,
+// (FX_FILTER_VARIANT: 64-query tiles, namespace fx::q64) and knn_filter_q128.hip
+// (128-query tiles, fx::q128) for small batches,
 // where a 256-query tile would re-read and multiply mostly padding.
 #ifndef FX_FILTER_BQ
 #define FX_FILTER_BQ 256
@@ -874,7 +875,7 @@ __device__ __forceinline__ void filter_flush_segments(uint32_t* seg, uint32_t* b
 // ------------------------------------------------------ tiled filter image
 #ifndef FX_FILTER_IMG2  // compiled into the 64-query and the 32-wide-K 256-query builds
                         // (the 64-wide-K h256 build measured 7 % slower on it)
-#define FX_FILTER_IMG2 (FX_FILTER_BQ == 64 || FX_FILTER_BK == 32)
+#define FX_FILTER_IMG2 (FX_FILTER_BQ <= 128 || FX_FILTER_BK == 32)
 #endif
 #ifndef FX_I2_SEG  // LDS append segment per query (0: a global atomic per lane and query);
                    // 64-query tiles only: 16 entries in the 256-query build (the most
@@ -1531,6 +1532,9 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
 namespace q64 {
 int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_q64.hip
 }
+namespace q128 {
+int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_q128.hip
+}
 namespace h256 {
 int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_h256.hip
 }
@@ -1552,9 +1556,11 @@ bool filter_ring() {
   return env != nullptr && atoi(env) != 0;
 }
 
-// Batches of <= 64 queries take the 64-query tiles (their Qh is padded to 64)
+// Batches of <= 64 queries take the 64-query tiles, 65..128 the 128-query ones
+// (their Qh is padded to 64 / 128, filter_query_pad)
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.nq <= 64) return q64::launch(a, metric, stream);
+  if (a.nq <= 128 && !filter_ring()) return q128::launch(a, metric, stream);
   // tiled images: K chunks of 32 (5.07-5.10 vs 5.48-5.49 ms for configs[2]
   // in the 64-wide h256 build, profiles/r02_filter_img_bk32.log)
   if (a.rowinfo != nullptr && image_tiled()) return q256::launch(a, metric, stream);
@@ -1568,7 +1574,7 @@ int filter_tile_rows(int dtype) {
   return dtype == FX_DTYPE_F16 || filter_ring() ? q256::ring::kBM : q256::fBM;
 }
 
-int filter_query_pad(int64_t nq) { return nq <= 64 ? 64 : 256; }
+int filter_query_pad(int64_t nq) { return nq <= 64 ? 64 : nq <= 128 && !filter_ring() ? 128 : 256; }
 int filter_dq(int d) { return (d + 63) / 64 * 64; }  // covers every variant's K chunk
 
 // Per query: the fp16 image scaled by 2^s (max|q| in [2^14, 2^15)), zero-padded

@@ -408,7 +408,10 @@ def test_batched_equals_unbatched(eng, monkeypatch):
     (257, 64, 9, 300, "1"),         # n < k, a single partial tile
     (40_000, 128, 2, 50, "0"),      # the smallest batch (64-query tiles)
     (40_000, 128, 64, 50, "1"),     # the largest 64-query tile
-    (40_000, 128, 65, 50, "0"),     # the smallest 256-query tile
+    (40_000, 128, 65, 50, "0"),     # the smallest 128-query tile
+    (40_000, 128, 128, 50, "0"),    # the largest 128-query tile
+    (40_000, 128, 129, 50, "0"),    # the smallest 256-query tile
+    (40_000, 128, 100, 50, "1"),    # the ring keeps 256-query tiles
 ])
 def test_batched_filter_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq, k, ring):
     """fp16-MFMA filter + exact rescoring == the single-query f32 scan, bit for
@@ -467,7 +470,7 @@ def test_batched_filter_sampling_plan_invariant(eng, monkeypatch, dtype):
 
 @pytest.mark.parametrize("metric", METRICS)
 @pytest.mark.parametrize("n,d,nq,k", [(120_000, 1536, 24, 1000), (20_003, 104, 64, 10),
-                                      (50_000, 768, 256, 100)])
+                                      (30_000, 200, 100, 40), (50_000, 768, 256, 100)])
 @pytest.mark.parametrize("ring", ["0", "1"])
 def test_batched_f16_corpus_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq, k, ring):
     """fp16 columns (configs[4]'s dtype) in a batch: the filter (register-
