@@ -1713,8 +1713,10 @@ __global__ void __launch_bounds__(256) image_tiled_kernel(const float* __restric
       const int k0 = 16 * ks + 8 * h;
       const bool ok = live && k0 < d;
       const float* p = xr + (k0 < d ? k0 : 0);
-      img_f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const img_f32x4*>(p));
-      img_f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const img_f32x4*>(p + 4));
+      // (plain loads: the line's other half is read at the next k-step, from L2;
+      // nontemporal loads had it refetched, 2x the bytes)
+      img_f32x4 a = *reinterpret_cast<const img_f32x4*>(p);
+      img_f32x4 b = *reinterpret_cast<const img_f32x4*>(p + 4);
       if (!ok) {
         a = img_f32x4(0.f);
         b = img_f32x4(0.f);
