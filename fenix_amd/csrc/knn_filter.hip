@@ -916,9 +916,6 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
   const int h = lane >> 5, l32 = lane & 31;
   const int64_t q0 = (int64_t)blockIdx.y * fBQ;
   const int nch = (a.d + fBK - 1) / fBK;
-#ifndef FX_I2_QPF
-#define FX_I2_QPF 1  // query chunks in flight per thread (2: two register sets)
-#endif
   const int ksteps = (a.d + 15) / 16;
   const int64_t ntile32 = (a.n + 31) / 32;
 #ifdef FX_FILTER_DIAG_BUILD
@@ -1013,43 +1010,14 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
     using B1 = std::integral_constant<int, 1>;
     FilterPreQ pq;
     XA xa0, xa1;
-#if FX_I2_QPF == 2
-    // query chunks two steps ahead in two register sets: at the start of step
-    // j, pq[(j + 1) & 1] holds chunk j + 1 and pq[j & 1] chunk j + 2 (in flight)
-    FilterPreQ pq2;
-    filter_load_q(pq, ad, o, 0, diag);
-    filter_load_q(pq2, ad, o, 1, diag);
-    load_x(xa0, 0);
-    load_x(xa1, 1);
-    store_q(pq, B0{});
-    filter_load_q(pq, ad, o, 2, diag);
-#else
     filter_load_q(pq, ad, o, 0, diag);
     load_x(xa0, 0);
     load_x(xa1, 1);
     store_q(pq, B0{});
     filter_load_q(pq, ad, o, 1, diag);
-#endif
     __syncthreads();
     // step c: multiply chunk c (registers xa[c & 1], query buffer c & 1),
     // store query chunk c + 1, load query chunk c + 2 and rows chunk c + 2
-#if FX_I2_QPF == 2
-    auto step = [&](int c, XA& xa, FilterPreQ& q, auto buf) {
-      constexpr int B = decltype(buf)::value;
-      compute(xa, buf);
-      store_q(q, std::integral_constant<int, B ^ 1>{});
-      filter_load_q(q, ad, o, c + 3, diag);
-      load_x(xa, c + 2);
-      __syncthreads();
-    };
-    int c = 0;
-    for (; c + 2 < nch; c += 2) {
-      step(c, xa0, pq2, B0{});
-      step(c + 1, xa1, pq, B1{});
-    }
-    const bool two = c + 1 < nch;
-    if (two) store_q(pq2, B1{});
-#else
     auto step = [&](int c, XA& xa, auto buf) {
       constexpr int B = decltype(buf)::value;
       compute(xa, buf);
@@ -1065,7 +1033,6 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
     }
     const bool two = c + 1 < nch;
     if (two) store_q(pq, B1{});
-#endif
     __syncthreads();
     compute(xa0, B0{});
     if (two) compute(xa1, B1{});
