@@ -963,6 +963,13 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
   for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
     const int64_t r0 = (a.tile_start + ti * a.tile_stride) * fBM;
     if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;
+#ifndef FX_I2_RPF
+#define FX_I2_RPF 1
+#endif
+    // this thread's row sum, loaded before the stream (not a dependent HBM
+    // load between the last MFMA and the epilogue's barrier)
+    float rsum = 0.f;
+    if (FX_I2_RPF && tid < fBM && r0 + tid < a.n) rsum = a.rowinfo[r0 + tid];
     // this wave's 32-row tile: its k-steps, one KB each (a tile past the end
     // reads zeros through the descriptor size)
     __amdgpu_buffer_rsrc_t xr;
@@ -1041,7 +1048,7 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
       const int lr = tid;
       const int64_t row = r0 + lr;
       bool ok = row < a.n;
-      const float s = ok ? a.rowinfo[row] : 0.f;
+      const float s = ok ? (FX_I2_RPF ? rsum : a.rowinfo[row]) : 0.f;
       if (ok && a.mask != nullptr) ok = (a.mask[row >> 5] >> (row & 31)) & 1u;
       float rv;
       if constexpr (METRIC == 0) {
