@@ -11,6 +11,10 @@ configs[3], 80M rows).
                     [--k K] [--nq Q] [--metric l2|cosine|inner_product]
                     [--dtype f32|f16] [--no-cpu-baseline]
 
+``--gpus N`` under a launcher (torch.distributed.run sets WORLD_SIZE) must
+equal the world size; without one, N > 1 starts the N ranks itself (a
+torch.distributed.run child, before this process touches a GPU).
+
 Prints ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
 """
 
@@ -31,7 +35,6 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md chip table
-MFMA_F32_PEAK_TFS = 157.3  # dense fp32 matrix peak (v_mfma_f32_32x32x2_f32), same table
 MFMA_F16_PEAK_TFS = 2500.0  # dense fp16/bf16 matrix peak, same table
 
 METRIC = "vectors/sec + %HBM roofline, 10M×768 f32 L2 kNN k=100 at 1/2/4/8 GPU"
@@ -127,23 +130,54 @@ QU8_SCALE = float(np.float32(4 * 3**0.5 / 127))
 QU8_ZP = 64
 
 
-def pmc_traffic(workload_tag):
-    """HBM bytes per scan launch from the committed rocprofv3 --pmc summary
-    (profiles/*pmc*.json, FETCH_SIZE x2 gfx950 correction already applied)."""
+def pmc_traffic(workload_tag, lib_sha):
+    """HBM bytes per scan launch from a committed rocprofv3 --pmc summary
+    (profiles/*pmc*.json, FETCH_SIZE x2 gfx950 correction already applied,
+    tools/summarize_profiles.py) of THIS build: the summary must carry the
+    SHA-256 of the library it measured, equal to the loaded one's, else the
+    traffic is unknown (None) — a kernel change makes an old pass stale."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             with open(path) as f:
                 rec = json.load(f)
         except (OSError, ValueError):
             continue
-        if rec.get("workload") == workload_tag and "hbm_bytes_per_launch" in rec:
+        if (rec.get("workload") == workload_tag and "hbm_bytes_per_launch" in rec
+                and rec.get("library_sha") == lib_sha):
             return float(rec["hbm_bytes_per_launch"])
     return None
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """``--gpus N`` without a launcher: start N ranks (one per GPU) as a
+    torch.distributed.run child on 127.0.0.1 and return its exit code.  Runs
+    before this process touches the GPU, and starts a child instead of
+    re-executing itself."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")).returncode
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per GPU; --dist-backend gloo lets several ranks share one GPU
@@ -213,6 +247,19 @@ def main():
             return eng.merge(gd, gr, k)
         return od, orow
 
+    # a batched f32 search streams the corpus's fp16 filter image, built once
+    # per corpus version: timed here, apart from the steps (reported in the
+    # record's filter_image field)
+    image_build_ms = None
+    if not qu8 and args.dtype == "f32":
+        b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        b0.record()
+        built = eng.filter_image(shard, nq, k, metric)[0] is not None
+        b1.record()
+        torch.cuda.synchronize()
+        if built:
+            image_build_ms = b0.elapsed_time(b1)
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -242,59 +289,42 @@ def main():
     value = total_rows * nq * args.steps / elapsed
     scan_bytes = n * d * esize + nq * d * 4
     tag = f"{n}x{d}_{args.dtype}_{args.metric}_k{k}_q{nq}"
-    traffic = pmc_traffic(tag)
-    # batched queries (f32): by default the fp16-MFMA bound filter + exact
-    # rescoring (knn_filter.hip), one HBM-bound pass over the corpus; with
-    # FX_BATCH_FILTER=0 the fp32-MFMA kernel (knn_batch.hip), MFMA-bound
-    # (fx_knn_scan takes the batched path from 2 queries, 8 without the filter:
-    # f32 with d % 4 == 0, f16 with d % 8 == 0 through the filter only)
-    filt_on = os.environ.get("FX_BATCH_FILTER", "1") != "0"
-    min_q = 2 if filt_on else 8  # capi.hip use_batched (FX_BATCH_MIN=1: single queries too)
-    if os.environ.get("FX_BATCH_MIN"):
-        min_q = int(os.environ["FX_BATCH_MIN"]) if int(os.environ["FX_BATCH_MIN"]) >= 1 else 2
-    batched = (os.environ.get("FX_BATCH", "1") != "0" and nq >= min_q
-               and ((args.dtype == "f32" and d % 4 == 0)
-                    or (args.dtype == "f16" and d % 8 == 0 and filt_on)))
-    filt = batched and filt_on
-    if batched and not filt:
-        flops = 2.0 * n * nq * d
-        roof = {
-            "bound": "mfma",
-            "achieved": flops / (scan_ms * 1e-3) / 1e12,
-            "peak": MFMA_F32_PEAK_TFS,
-            "unit": "TFLOP/s",
-            "traffic": traffic,
-            "kernel": "fx::batch_kernel (fp32 MFMA GEMM + threshold filter), all sample phases",
-            "kernel_ms": scan_ms,
-            "flops_per_launch": flops,
-        }
+    traffic = pmc_traffic(tag, _lib.library_sha())
+    # batched queries: the fp16-MFMA bound filter + exact rescoring
+    # (knn_filter.hip), one HBM-bound pass over the corpus (capi.hip
+    # use_batched: from "batch_min_queries" queries, f32 rows with d % 4 == 0,
+    # f16 rows with d % 8 == 0)
+    min_q = max(1, _lib.get_option("batch_min_queries"))
+    batched = (_lib.get_option("batched") != 0 and nq >= min_q and not qu8
+               and ((args.dtype == "f32" and d % 4 == 0) or (args.dtype == "f16" and d % 8 == 0)))
+    filt = batched
+    if filt and args.dtype == "f32" and id(x) in eng._images:
+        # the phases stream the fp16 image and its row sums instead of the
+        # f32 rows: those are the bytes of the pass (the rescoring reads a
+        # few thousand f32 rows per query on top)
+        scan_bytes = n * d * 2 + n * 4 + nq * d * 4
+    achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
+    if filt:
+        kname = ("fx::filter_kernel (fp16-MFMA bound filter, all sample phases) "
+                 "+ exact rescoring of the candidates")
+    elif qu8:
+        kname = "fx::scan_kernel<uint8> (quint8 codes dequantised in registers) + merge"
     else:
-        if filt and args.dtype == "f32" and id(x) in eng._images:
-            # the phases stream the fp16 image and its row sums instead of the
-            # f32 rows: those are the bytes of the pass (the rescoring reads a
-            # few thousand f32 rows per query on top)
-            scan_bytes = n * d * 2 + n * 4 + nq * d * 4
-        achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
-        if filt:
-            kname = ("fx::filter_kernel (fp16-MFMA bound filter, all sample phases) "
-                     "+ exact rescoring of the candidates")
-        elif qu8:
-            kname = "fx::scan_kernel<uint8> (quint8 codes dequantised in registers) + merge"
-        else:
-            kname = "fx::scan_kernel (fused distance + per-wave top-k)"
-        roof = {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "traffic": traffic,
-            "kernel": kname,
-            "kernel_ms": scan_ms,
-            "bytes_per_launch": scan_bytes,
-        }
-        if filt:  # the GEMM the filter evaluates, against the dense fp16 MFMA peak
-            roof["mfma_tflops"] = 2.0 * n * nq * d / (scan_ms * 1e-3) / 1e12
-            roof["mfma_peak_tflops"] = MFMA_F16_PEAK_TFS
+        kname = "fx::scan_kernel (fused distance + per-wave top-k)"
+    roof = {
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "traffic": traffic,
+        "kernel": kname,
+        "kernel_ms": scan_ms,
+        "bytes_per_launch": scan_bytes,
+        "library_sha": _lib.library_sha(),
+    }
+    if filt:  # the GEMM the filter evaluates, against the dense fp16 MFMA peak
+        roof["mfma_tflops"] = 2.0 * n * nq * d / (scan_ms * 1e-3) / 1e12
+        roof["mfma_peak_tflops"] = MFMA_F16_PEAK_TFS
     roof["frac"] = roof["achieved"] / roof["peak"]
     image = eng._images.get(id(x)) if filt and args.dtype == "f32" else None
 
@@ -333,8 +363,11 @@ def main():
             # image (fx_filter_image, built in the warmup; candidates rescored
             # from the f32 rows, results bit-identical to the f32 scan)
             **({"filter_image": {"bytes": int(image[1].numel()) * 2 + int(image[2].numel()) * 4,
+                                 "build_ms": image_build_ms,
                                  "note": "fp16 image + row sums of squares resident beside "
-                                         "the f32 corpus; FENIX_AMD_FILTER_IMAGE=0 disables"}}
+                                         "the f32 corpus, built once per corpus version "
+                                         "(build_ms, not in ms_per_step); "
+                                         "FENIX_AMD_FILTER_IMAGE=0 disables"}}
                if image is not None else {}),
             "roofline": roof,
             "cpu_baseline": cpu,

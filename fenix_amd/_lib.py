@@ -10,9 +10,12 @@ shapes -> ``NotImplementedError``, HIP failures -> ``RuntimeError``.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import hashlib
 import os
 import threading
+from typing import Iterator
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FENIX_AMD_LIB") or os.path.join(HERE, "lib", "libfenix_knn.so")
@@ -71,7 +74,15 @@ SYMBOLS = (
     "fx_comm_init_all",
     "fx_comm_destroy",
     "fx_allgather_topk",
+    "fx_set_option",
+    "fx_get_option",
+    "fx_host_sync_count",
 )
+
+# process options of the library (fx_set_option, include/fenix_knn.h): the
+# first two are user switches, the rest test switches
+OPTIONS = ("batched", "batch_min_queries", "batch_cap", "batch_sample_ratio", "force_fallback",
+           "scan_interleave", "q8_dma")
 
 _lock = threading.Lock()
 _lib = None
@@ -186,6 +197,12 @@ def load() -> ctypes.CDLL:
         pvp = ctypes.POINTER(vp)
         L.fx_allgather_topk.argtypes = [vp, pvp, pvp, i64, i64, pvp, pvp, pvp]
         L.fx_allgather_topk.restype = ci
+        L.fx_set_option.argtypes = [ctypes.c_char_p, i64]
+        L.fx_set_option.restype = ci
+        L.fx_get_option.argtypes = [ctypes.c_char_p, ctypes.POINTER(i64)]
+        L.fx_get_option.restype = ci
+        L.fx_host_sync_count.argtypes = []
+        L.fx_host_sync_count.restype = ctypes.c_uint64
         _lib = L
         return L
 
@@ -262,3 +279,48 @@ def search_ex_workspace_bytes(corpus: "Corpus", nrows: int, nq: int, k: int) -> 
     check(load().fx_knn_search_ex_workspace_bytes(ctypes.byref(corpus), nrows, nq, k,
                                                   ctypes.byref(out)))
     return int(out.value)
+
+
+def set_option(name: str, value: int) -> None:
+    """fx_set_option: a process-wide library option (OPTIONS)."""
+    check(load().fx_set_option(name.encode(), int(value)))
+
+
+def get_option(name: str) -> int:
+    out = ctypes.c_int64(0)
+    check(load().fx_get_option(name.encode(), ctypes.byref(out)))
+    return int(out.value)
+
+
+@contextlib.contextmanager
+def options(**kw: int) -> Iterator[None]:
+    """Set library options for the duration of a block (tests, tools)."""
+    old = {k: get_option(k) for k in kw}
+    try:
+        for k, v in kw.items():
+            set_option(k, v)
+        yield
+    finally:
+        for k, v in old.items():
+            set_option(k, v)
+
+
+def host_sync_count() -> int:
+    """fx_host_sync_count: host-blocking synchronisations inside the library."""
+    return int(load().fx_host_sync_count())
+
+
+_sha = None
+
+
+def library_sha() -> str:
+    """SHA-256 (first 16 hex digits) of the loaded shared library file: stamps
+    profiles so a measurement is matched to the build it came from."""
+    global _sha
+    if _sha is None:
+        h = hashlib.sha256()
+        with open(LIB_PATH, "rb") as f:
+            for blk in iter(lambda: f.read(1 << 20), b""):
+                h.update(blk)
+        _sha = h.hexdigest()[:16]
+    return _sha

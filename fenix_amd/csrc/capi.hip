@@ -3,7 +3,9 @@
 #include <stdarg.h>
 #include <stdlib.h>
 #include <stdio.h>
+#include <string.h>
 
+#include <atomic>
 #include <map>
 #include <set>
 #include <tuple>
@@ -34,6 +36,32 @@ int check_launch(const char* what) {
 }
 
 static std::mutex g_mu;
+
+// ----------------------------------------------------------------- options --
+static const char* const kOptNames[kOptCount] = {
+    "batched", "batch_min_queries", "batch_cap", "batch_sample_ratio",
+    "force_fallback", "scan_interleave", "q8_dma"};
+static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}};
+
+int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
+
+static int option_index(const char* name) {
+  if (name == nullptr) return -1;
+  for (int i = 0; i < kOptCount; ++i)
+    if (strcmp(name, kOptNames[i]) == 0) return i;
+  return -1;
+}
+
+#ifdef FX_DIAG_BUILD
+int diag_env(const char* name, int dflt) {
+  const char* env = getenv(name);
+  return env != nullptr ? atoi(env) : dflt;
+}
+#endif
+
+// host-blocking synchronisations performed (fx_host_sync_count); searches
+// perform none, and any added one must go through host_sync
+static std::atomic<uint64_t> g_host_syncs{0};
 
 int device_cus(int* out) {
   int dev = 0;
@@ -159,8 +187,7 @@ static constexpr int64_t kLargeMaxK = 0x7fffffffll;
 //            row subset is), so it keeps ~cap/4 candidates per query;
 //   last:    every row with the last threshold -> final select.
 // A query whose final candidates overflow `cap` is recomputed exactly by the
-// single-query scan (fx_knn_reduce synchronises the stream once to check).
-static constexpr int64_t kBatchMinQ = 2;  // 2 queries: 6.5 ms vs 2 x 4.5 ms (10Mx768)
+// single-query scan, gated on the device (fx_knn_reduce: no host sync).
 static constexpr int64_t kListLen = 4096;  // candidate buffer viewed as lists
 
 struct BatchLayout {
@@ -174,21 +201,17 @@ struct BatchLayout {
       total;
 };
 
-// FX_BATCH_FILTER=0 selects the fp32-MFMA batch kernel (knn_batch.hip)
-static bool use_filter() {
-  const char* env = getenv("FX_BATCH_FILTER");
-  return env == nullptr || atoi(env) != 0;
-}
+// The fp16-MFMA filter (knn_filter.hip).  Diagnostic builds keep the
+// rejected fp32-MFMA batch kernel (knn_batch.hip) behind FX_BATCH_FILTER=0.
+static bool use_filter() { return diag_env("FX_BATCH_FILTER", 1) != 0; }
 
 static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool aligned) {
-  if (const char* env = getenv("FX_BATCH")) {
-    if (atoi(env) == 0) return false;
-  }
-  int64_t min_q = kBatchMinQ;
+  if (option(kOptBatched) == 0) return false;
+  // 2 queries: 6.5 ms vs 2 x 4.5 ms (10Mx768); "batch_min_queries" = 1 also
+  // sends single queries through the filter (with a filter image that halves
+  // their bytes; the default keeps the exact scan)
+  int64_t min_q = option(kOptBatchMinQ) >= 1 ? option(kOptBatchMinQ) : 2;
   if (!use_filter()) min_q = 8;  // the fp32-MFMA kernel breaks even with scans at ~8 queries
-  // FX_BATCH_MIN=1 also sends single queries through the filter (with a
-  // filter image that halves their bytes; the default keeps the exact scan)
-  if (const char* env = getenv("FX_BATCH_MIN")) min_q = atoll(env) >= 1 ? atoll(env) : 2;
   if (nq < min_q || !aligned) return false;
   // the rescoring repeats the scan's 16-B slot order: f32 rows need d % 4 == 0,
   // f16 rows d % 8 == 0 (and the fp16 filter: the fp32-MFMA kernel reads f32 only)
@@ -200,18 +223,15 @@ static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, 
   b->filter = use_filter();
   const int64_t tr = b->filter ? filter_tile_rows(dtype) : batch_tile_rows();
   b->cap = 64 * k > 16384 ? 64 * k : 16384;
-  if (const char* env = getenv("FX_BATCH_CAP")) {  // test knob: small buffers
-    const int64_t c = atoll(env);
-    if (c >= 16 * k) b->cap = c;
-  }
+  if (option(kOptBatchCap) >= 16 * k) b->cap = option(kOptBatchCap);  // test: small buffers
   b->cap = (b->cap + kListLen - 1) / kListLen * kListLen;
   b->tiles = (n + tr - 1) / tr;
   // nested samples: phase i scans every stride_i-th tile, each stride a
   // multiple of the next, so every sample contains the previous one and has
   // at least k rows under the previous threshold; ~cap/4 appends per query.
   int64_t r = b->cap / (4 * k);  // >= 16 for k <= 1024
-  if (const char* env = getenv("FX_BATCH_R")) {  // tuning knob: denser samples (never sparser)
-    const int64_t v = atoll(env);
+  {  // test switch: denser samples (never sparser)
+    const int64_t v = option(kOptBatchRatio);
     if (v >= 2 && v < r) r = v;
   }
   int64_t strides[16];
@@ -267,7 +287,8 @@ struct SearchLayout {
   LargeLayout lg;
   bool batched;
   BatchLayout batch;
-  size_t single_off;  // batched: workspace of the single-query fallback
+  size_t single_off;   // batched: workspace of the overflow fallback
+  int64_t fb_queries;  // batched: queries per fallback round (scan + merge over fb_queries)
 };
 
 static int plan_single(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
@@ -294,37 +315,57 @@ static int plan_large_search(int64_t n, int64_t d, int dtype, int64_t nq, int me
   return FX_OK;
 }
 
+// The overflow fallback of the batched path runs the single-query plan over
+// rounds of fq queries; its candidate lists take at most this many bytes
+// (fq = 256 at 10M rows and k = 100, 32 at k = 1 000).
+static constexpr size_t kFallbackListBytes = (size_t)256 << 20;
+
+static int plan_fallback(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
+                         bool aligned, SearchLayout* s, int64_t* fq) {
+  int rc = plan_single(n, d, dtype, 1, k, metric, aligned, s);
+  if (rc) return rc;
+  int64_t f = (int64_t)(kFallbackListBytes / (s->total > 0 ? s->total : 1));
+  if (f > nq) f = nq;
+  if (f > 65535) f = 65535;
+  if (f < 1) f = 1;
+  *fq = f;
+  return f == 1 ? FX_OK : plan_single(n, d, dtype, f, k, metric, aligned, s);
+}
+
 static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
                        bool aligned, SearchLayout* s) {
   if (k > kMaxK) return plan_large_search(n, d, dtype, nq, metric, aligned, s);
   if (!use_batched(nq, dtype, metric, d, aligned)) {
     return plan_single(n, d, dtype, nq, k, metric, aligned, s);
   }
-  // the single-query plan (nq = 1) serves overflowing queries
-  int rc = plan_single(n, d, dtype, 1, k, metric, aligned, s);
+  // the single-query plan over fb_queries queries serves overflowing queries
+  int64_t fq = 1;
+  int rc = plan_fallback(n, d, dtype, nq, k, metric, aligned, s, &fq);
   if (rc) return rc;
   const size_t single_total = s->total;
   rc = plan_batched(n, d, dtype, nq, k, &s->batch);
   if (rc) return rc;
   s->batched = true;
+  s->fb_queries = fq;
   s->single_off = s->batch.total;
   s->total = s->batch.total + single_total;
   return FX_OK;
 }
 
 
-// one query through the single-query scan + merge (batched-path fallback)
-static int single_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
-                         const float* query, int metric, int64_t k, const uint32_t* mask,
-                         void* ws, size_t ws_bytes, float* out_dist, int64_t* out_row,
-                         hipStream_t st) {
-  SearchLayout s;
-  int rc = plan_single(n, d, dtype, 1, k, metric, ((uintptr_t)corpus % 16) == 0, &s);
-  if (rc) return rc;
-  if (ws_bytes < s.total) {
-    set_error("fallback workspace too small: %zu < %zu", ws_bytes, s.total);
-    return FX_EINVAL;
-  }
+// Batched-path fallback: the exact single-query scan + merge of every query
+// whose final candidates overflowed the buffer (count[q] > gate_cap; all of
+// them when gate_cap < 0), in rounds of s.fb_queries.  Decided on the device:
+// each workgroup reads its query's count and returns at once when it did not
+// overflow, so nothing waits for the host; the merge writes only the
+// recomputed queries' results.
+static int fallback_search(const SearchLayout& s, const void* corpus, int dtype, int64_t n,
+                           int64_t d, int64_t row_base, const float* queries, int64_t nq,
+                           int metric, int64_t k, const uint32_t* mask, const uint32_t* count,
+                           int64_t gate_cap, char* ws, float* out_dist, int64_t* out_row,
+                           hipStream_t st) {
+  (void)dtype;
+  (void)metric;
   ScanArgs a = {};
   a.X = corpus;
   a.n = n;
@@ -336,12 +377,19 @@ static int single_search(const void* corpus, int dtype, int64_t n, int64_t d, in
   a.cap = s.scan.cap;
   a.qbytes = s.scan.qbytes;
   a.mode = kModeTopk;
-  a.q = query;
   a.out_lists = reinterpret_cast<uint64_t*>(ws);
-  rc = launch_scan(s.scan, a, 1, st);
-  if (rc) return rc;
-  return run_merge(s.merge, a.out_lists, 1, k, reinterpret_cast<char*>(ws) + s.lists_bytes,
-                   out_dist, out_row, st);
+  a.gate_cap = gate_cap;
+  for (int64_t q0 = 0; q0 < nq; q0 += s.fb_queries) {
+    const int64_t qn = (nq - q0) < s.fb_queries ? (nq - q0) : s.fb_queries;
+    a.q = queries + (size_t)q0 * d;
+    a.gate = count + (size_t)q0 * kCountStride;
+    int rc = launch_scan(s.scan, a, qn, st);
+    if (rc) return rc;
+    rc = run_merge(s.merge, a.out_lists, qn, k, ws + s.lists_bytes, out_dist + (size_t)q0 * k,
+                   out_row + (size_t)q0 * k, st, nullptr, a.gate, gate_cap);
+    if (rc) return rc;
+  }
+  return FX_OK;
 }
 
 // fp16 filter phases (knn_filter.hip).  Sampling phases append the UPPER
@@ -399,7 +447,7 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
     a.cand = cand;
     a.cand_ub = last ? cand_ub : nullptr;
     a.cap = (int)b.cap;
-    if (const char* dg = getenv("FX_FILTER_DIAG")) a.diag = atoi(dg);
+    a.diag = diag_env("FX_FILTER_DIAG", 0);
     rc = launch_filter(a, metric, st);
     if (rc) return rc;
     // the k-th upper bound of this phase's candidates: next threshold
@@ -415,6 +463,7 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
                         metric, thr, st);
 }
 
+#ifdef FX_DIAG_BUILD
 static int batched_phases(const BatchLayout& b, const float* X, int64_t n, int64_t d,
                           int64_t row_base, const float* Q, int64_t nq, int metric, int64_t k,
                           const uint32_t* mask, char* w, hipStream_t st) {
@@ -469,6 +518,7 @@ static int batched_phases(const BatchLayout& b, const float* X, int64_t n, int64
   }
   return FX_OK;
 }
+#endif  // FX_DIAG_BUILD
 
 }  // namespace fx
 
@@ -476,9 +526,31 @@ using namespace fx;
 
 extern "C" {
 
-int fx_version(void) { return 101; }
+int fx_version(void) { return 102; }
 
 const char* fx_last_error(void) { return g_err; }
+
+int fx_set_option(const char* name, int64_t value) {
+  const int i = option_index(name);
+  if (i < 0) {
+    set_error("unknown option %s", name ? name : "(null)");
+    return FX_EINVAL;
+  }
+  g_opts[i].store(value, std::memory_order_relaxed);
+  return FX_OK;
+}
+
+int fx_get_option(const char* name, int64_t* out) {
+  const int i = option_index(name);
+  if (i < 0 || out == nullptr) {
+    set_error("unknown option %s", name ? name : "(null)");
+    return FX_EINVAL;
+  }
+  *out = g_opts[i].load(std::memory_order_relaxed);
+  return FX_OK;
+}
+
+uint64_t fx_host_sync_count(void) { return g_host_syncs.load(std::memory_order_relaxed); }
 
 int fx_device_count(int* out) {
   int c = 0;
@@ -576,8 +648,10 @@ static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_
       return filter_phases(s.batch, corpus, dtype, img ? image : nullptr, rowinfo, n, d, row_base,
                            queries, nq, metric, k, mask, reinterpret_cast<char*>(ws), st);
     }
+#ifdef FX_DIAG_BUILD
     return batched_phases(s.batch, reinterpret_cast<const float*>(corpus), n, d, row_base,
                           queries, nq, metric, k, mask, reinterpret_cast<char*>(ws), st);
+#endif
   }
   if (s.large) {
     ScanArgs a = {};
@@ -713,27 +787,12 @@ int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
   const uint64_t* cand = reinterpret_cast<const uint64_t*>(w + b.off_cand);
   rc = run_merge(b.merge, cand, nq, k, w + b.off_merge, out_dist, out_row, st);
   if (rc) return rc;
-  // queries whose candidates overflowed `cap`: recompute exactly, one by one
-  std::vector<uint32_t> counts((size_t)nq);
-  hipError_t e = hipMemcpy2DAsync(counts.data(), 4, w + b.off_count, 4 * kCountStride, 4,
-                                  (size_t)nq, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) {
-    set_error("batched overflow check: %s", hipGetErrorString(e));
-    return FX_EHIP;
-  }
-  void* sws = w + s.single_off;
-  const size_t sws_bytes = ws_bytes - s.single_off;
-  // FX_BATCH_FORCE_FALLBACK=1 (test knob) treats every query as overflowed
-  const char* force = getenv("FX_BATCH_FORCE_FALLBACK");
-  const bool all = force != nullptr && atoi(force) != 0;
-  for (int64_t q = 0; q < nq; ++q) {
-    if (!all && counts[(size_t)q] <= (uint32_t)b.cap) continue;
-    rc = single_search(corpus, dtype, n, d, row_base, queries + q * d, metric, k, mask, sws,
-                       sws_bytes, out_dist + q * k, out_row + q * k, st);
-    if (rc) return rc;
-  }
-  return FX_OK;
+  // queries whose candidates overflowed `cap`: recomputed exactly, gated on
+  // the device ("force_fallback" (test switch): every query)
+  const int64_t gate_cap = option(kOptForceFallback) != 0 ? -1 : b.cap;
+  return fallback_search(s, corpus, dtype, n, d, row_base, queries, nq, metric, k, mask,
+                         reinterpret_cast<const uint32_t*>(w + b.off_count), gate_cap,
+                         w + s.single_off, out_dist, out_row, st);
 }
 
 int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,

@@ -12,6 +12,28 @@ constexpr int kModeDist = 1;
 // counter in its own cache line, so the L2 channels serialise fewer atomics.
 constexpr int kCountStride = 32;
 
+// Process-wide options (fx_set_option, include/fenix_knn.h); relaxed atomics.
+enum Option : int {
+  kOptBatched,
+  kOptBatchMinQ,
+  kOptBatchCap,
+  kOptBatchRatio,
+  kOptForceFallback,
+  kOptScanInterleave,
+  kOptQ8Dma,
+  kOptCount
+};
+int64_t option(Option o);
+
+// Diagnostic builds for tools/ (make diag: -DFX_DIAG_BUILD) read a few
+// variant and tuning switches from the environment; the product library
+// compiles the rejected variants out and takes the defaults.
+#ifdef FX_DIAG_BUILD
+int diag_env(const char* name, int dflt);
+#else
+constexpr int diag_env(const char*, int dflt) { return dflt; }
+#endif
+
 struct ScanArgs {
   const void* X;          // [n][d] corpus shard
   int64_t n;
@@ -32,6 +54,11 @@ struct ScanArgs {
   // block steps of 16U rows dealt round-robin over the grid.  Bit 1: no
   // software pipeline (one tile per wave in flight).  Set by launch_scan.
   int interleave;
+  // Device-side gate (the batched path's overflow fallback): when non-null, a
+  // workgroup of query qi returns at once unless gate[qi * kCountStride] >
+  // gate_cap (gate_cap < 0: every query runs).
+  const uint32_t* gate;
+  int64_t gate_cap;
 };
 
 typedef void (*ScanKernelFn)(ScanArgs);
@@ -62,9 +89,11 @@ struct MergePlan {
 int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p);
 // out_dist/out_row may be null; out_kth (optional) receives each query's k-th
 // smallest composite (kEmpty if fewer than k candidates).
+// gate/gate_cap: as ScanArgs::gate, per query of the merge.
 int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, void* ws,
               float* out_dist, int64_t* out_row, hipStream_t stream,
-              uint64_t* out_kth = nullptr);
+              uint64_t* out_kth = nullptr, const uint32_t* gate = nullptr,
+              int64_t gate_cap = 0);
 
 // Batched queries (knn_batch.hip): fp32 MFMA GEMM + threshold filter.
 struct BatchArgs {
@@ -118,7 +147,7 @@ struct FilterArgs {
   int cap;
   const float* rowinfo;   // [n] row sums of squares of the f32 rows when X is their fp16
                           // filter image (dtype F16), NaN = forced; null otherwise
-  int diag;               // FX_FILTER_DIAG (profiling only): 1 no appends, 2 no epilogue,
+  int diag;               // FX_FILTER_DIAG (diagnostic builds only): 1 no appends, 2 no epilogue,
                           // 4 no MFMA, 8 no query loads, 16 no LDS stores,
                           // 32 no append atomics, 64 no append stores
 };

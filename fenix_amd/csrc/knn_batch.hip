@@ -29,6 +29,10 @@
 
 namespace fx {
 
+// The fp32-MFMA batch kernel was replaced by the fp16-MFMA filter
+// (knn_filter.hip, 4-7x faster); it stays in diagnostic builds (tools/).
+// The query norms and the exact rescoring below serve the filter.
+#ifdef FX_DIAG_BUILD
 #ifndef FX_BATCH_BQ
 #define FX_BATCH_BQ 256  // queries per block: 256 (110 KB LDS, 1 block/CU) or 128 (74 KB, 2)
 #endif
@@ -257,7 +261,9 @@ int launch_batch(const BatchArgs& a, int metric, hipStream_t stream) {
   return check_launch("batch_kernel");
 }
 
-int batch_tile_rows() { return kBM; }
+#endif  // FX_DIAG_BUILD
+
+int batch_tile_rows() { return 128; }
 
 // cosine: max(||q||, 1e-12) per query (F.normalize eps, coder.py:43-44);
 // L2 (mode 1): sum of squares for the expansion

@@ -918,7 +918,7 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
   const int nch = (a.d + fBK - 1) / fBK;
   const int ksteps = (a.d + 15) / 16;
   const int64_t ntile32 = (a.n + 31) / 32;
-#ifdef FX_FILTER_DIAG_BUILD
+#ifdef FX_DIAG_BUILD
   const int diag = a.diag;
 #else
   constexpr int diag = 0;
@@ -1127,7 +1127,7 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
   const int tid = threadIdx.x;
   filter_query_table<METRIC>(a, (int64_t)blockIdx.y * fBQ, sh->qtab, sh->qab, tid, fThreads);
   // (the first tile's barriers order these writes before the epilogue reads)
-#ifdef FX_FILTER_DIAG_BUILD
+#ifdef FX_DIAG_BUILD
   const int diag = a.diag;
 #else
   constexpr int diag = 0;
@@ -1140,6 +1140,7 @@ __global__ void __launch_bounds__(fThreads, fWaves * FX_FILTER_BPC / 4) filter_k
     filter_tiles<XT, METRIC, IMG, false>(a, smem, tid, diag);
 }
 
+#ifdef FX_DIAG_BUILD  // rejected variant, tools/ builds only
 // ------------------------------------------------------------- LDS-DMA ring
 //
 // The same filter with every operand staged by LDS-DMA (buffer_load ... lds):
@@ -1457,6 +1458,7 @@ static int launch_ring(const FilterArgs& a, int metric, hipStream_t stream) {
   }
   return check_launch("ring_kernel");
 }
+#endif  // FX_DIAG_BUILD
 
 int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.num_tiles <= 0) return FX_OK;
@@ -1469,6 +1471,7 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
     return FX_EUNSUPPORTED;
 #endif
   }
+#ifdef FX_DIAG_BUILD
   if (filter_ring()) {
     if (a.rowinfo != nullptr) {
       if (!f16) {
@@ -1479,6 +1482,7 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
     }
     return f16 ? launch_ring<_Float16>(a, metric, stream) : launch_ring<float>(a, metric, stream);
   }
+#endif
   const size_t smem = sizeof(FilterShared);
   // (the 256-query compilation serves f32 rows, h256 fp16 rows, q64 both)
 #if FX_FILTER_ROWS & 1
@@ -1488,7 +1492,11 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
 #endif
 #if FX_FILTER_ROWS & 2
 #define FX_F16_KERNEL(m) (const void*)filter_kernel<_Float16, m, false>
+#ifdef FX_DIAG_BUILD  // row-major images (rejected: the tiled image is 7-10 % faster)
 #define FX_IMG_KERNEL(m) (const void*)filter_kernel<_Float16, m, true>
+#else
+#define FX_IMG_KERNEL(m) nullptr
+#endif
 #else
 #define FX_F16_KERNEL(m) nullptr
 #define FX_IMG_KERNEL(m) nullptr
@@ -1546,22 +1554,15 @@ namespace h256 {
 int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_h256.hip
 }
 
-// The register-staged kernel by default (measured faster for both row types:
-// 8.5 vs 10.1 ms for configs[2]; see DESIGN.md for fp16); FX_FILTER_RING=1
-// selects the LDS-DMA ring.
-// Filter images in MFMA fragment order (filter_img2_kernel) by default;
-// FX_IMAGE_TILED=0 selects row-major images (the register-staged kernels'
-// IMG path).  Read when an image is built and when it is searched: both must
-// happen under the same setting.
-bool image_tiled() {
-  const char* env = getenv("FX_IMAGE_TILED");
-  return env == nullptr || atoi(env) != 0;
-}
+// The register-staged kernel (measured faster for both row types: 8.5 vs
+// 10.1 ms for configs[2]; see DESIGN.md for fp16) and filter images in MFMA
+// fragment order (filter_img2_kernel).  Diagnostic builds keep the rejected
+// LDS-DMA ring (FX_FILTER_RING=1) and row-major images (FX_IMAGE_TILED=0;
+// read when an image is built and when it is searched: both must happen
+// under the same setting).
+bool image_tiled() { return diag_env("FX_IMAGE_TILED", 1) != 0; }
 
-bool filter_ring() {
-  const char* env = getenv("FX_FILTER_RING");
-  return env != nullptr && atoi(env) != 0;
-}
+bool filter_ring() { return diag_env("FX_FILTER_RING", 0) != 0; }
 
 // Batches of <= 64 queries take the 64-query tiles, 65..128 the 128-query ones
 // (their Qh is padded to 64 / 128, filter_query_pad)
@@ -1578,7 +1579,11 @@ int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
 // rows per tile of the kernel launch_filter picks for the dtype (the 64-query
 // variant tiles rows like the 256-query one)
 int filter_tile_rows(int dtype) {
-  return dtype == FX_DTYPE_F16 || filter_ring() ? q256::ring::kBM : q256::fBM;
+  (void)dtype;
+#ifdef FX_DIAG_BUILD
+  static_assert(q256::ring::kBM == q256::fBM, "one tile height for every filter kernel");
+#endif
+  return q256::fBM;
 }
 
 int filter_query_pad(int64_t nq) { return nq <= 64 ? 64 : nq <= 128 && !filter_ring() ? 128 : 256; }
@@ -1666,6 +1671,7 @@ int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int 
 // change.  One wave per row, grid-stride.
 typedef float img_f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 img_f16x4 __attribute__((ext_vector_type(4)));
+#ifdef FX_DIAG_BUILD  // row-major images (FX_IMAGE_TILED=0)
 __global__ void __launch_bounds__(256) image_kernel(const float* __restrict__ X, int64_t n, int d,
                                                     _Float16* __restrict__ img,
                                                     float* __restrict__ rowinfo) {
@@ -1692,6 +1698,7 @@ __global__ void __launch_bounds__(256) image_kernel(const float* __restrict__ X,
     if (lane == 0) rowinfo[r] = (s <= 3.4e38f && m < 65520.f) ? s : __builtin_nanf("");
   }
 }
+#endif  // FX_DIAG_BUILD
 
 // The image in MFMA fragment order (FX_IMAGE_TILED): one wave per 32-row
 // tile, grid-stride.  Each k-step, lane l reads components 16 s + 8 (l / 32)
@@ -1757,11 +1764,15 @@ int launch_image(const float* X, int64_t n, int d, void* img, float* rowinfo,
                        reinterpret_cast<_Float16*>(img), rowinfo);
     return check_launch("image_tiled_kernel");
   }
+#ifdef FX_DIAG_BUILD
   int64_t blocks = (n + 3) / 4;
   if (blocks > (int64_t)cus * 32) blocks = (int64_t)cus * 32;
   hipLaunchKernelGGL(image_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, n, d,
                      reinterpret_cast<_Float16*>(img), rowinfo);
   return check_launch("image_kernel");
+#else
+  return FX_EUNSUPPORTED;  // (unreachable: image_tiled() is constant)
+#endif
 }
 
 #endif  // FX_FILTER_VARIANT

@@ -26,7 +26,7 @@ __global__ void __launch_bounds__(kMergeThreads)
     merge_kernel(const uint64_t* __restrict__ in, int64_t nlists, int kin, int64_t G, int k,
                  int P2, uint64_t* __restrict__ out_lists, float* __restrict__ out_dist,
                  int64_t* __restrict__ out_row, uint64_t* __restrict__ out_kth,
-                 int final_level) {
+                 int final_level, const uint32_t* __restrict__ gate, int64_t gate_cap) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   MergeShared* ms = reinterpret_cast<MergeShared*>(smem);
   uint64_t* res = reinterpret_cast<uint64_t*>(smem + sizeof(MergeShared));
@@ -35,6 +35,8 @@ __global__ void __launch_bounds__(kMergeThreads)
 
   const int tid = threadIdx.x;
   const int q = blockIdx.y;
+  // the batched path's overflow fallback merges only the recomputed queries
+  if (gate != nullptr && (int64_t)gate[(size_t)q * kCountStride] <= gate_cap) return;
   const int64_t l0 = (int64_t)blockIdx.x * G;
   const int nl = (int)((nlists - l0) < G ? (nlists - l0) : G);
   const int m = nl * kin;
@@ -144,8 +146,8 @@ int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p)
     const int64_t target = 8 * klen > 3200 ? 8 * klen : 3200;
     int64_t G = (target + klen - 1) / klen;
     if (G * klen > kMergeEntries) G = kMergeEntries / klen;
-    if (const char* env = getenv("FX_MERGE_GROUP")) {  // tuning knob (tools/microbench.py)
-      const int64_t g = atoll(env);
+    {  // FX_MERGE_GROUP: tuning knob of diagnostic builds (tools/microbench.py)
+      const int64_t g = diag_env("FX_MERGE_GROUP", 0);
       if (g >= 2 && g * klen <= kMergeEntries) G = g;
     }
     if (G < 2) G = 2;
@@ -170,7 +172,8 @@ int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p)
 }
 
 int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, void* ws,
-              float* out_dist, int64_t* out_row, hipStream_t stream, uint64_t* out_kth) {
+              float* out_dist, int64_t* out_row, hipStream_t stream, uint64_t* out_kth,
+              const uint32_t* gate, int64_t gate_cap) {
   const int P2 = next_pow2((int)k);
   uint64_t* bufs[2] = {reinterpret_cast<uint64_t*>(ws),
                        reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + p.ws_bytes / 2)};
@@ -193,8 +196,9 @@ int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, voi
       float* od = out_dist ? out_dist + (size_t)q0 * k : nullptr;
       int64_t* orow = out_row ? out_row + (size_t)q0 * k : nullptr;
       uint64_t* okth = out_kth ? out_kth + q0 : nullptr;
+      const uint32_t* gq = gate ? gate + (size_t)q0 * kCountStride : nullptr;
       hipLaunchKernelGGL(merge_kernel, grid, dim3(kMergeThreads), smem, stream, src, lists,
-                         (int)klen, G, (int)k, P2, dq, od, orow, okth, fin ? 1 : 0);
+                         (int)klen, G, (int)k, P2, dq, od, orow, okth, fin ? 1 : 0, gq, gate_cap);
       int rc = check_launch("merge_kernel");
       if (rc) return rc;
     }

@@ -455,6 +455,8 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
 
   float* q_lds = reinterpret_cast<float*>(smem);
   const int qi = blockIdx.y;
+  // the batched path's overflow fallback: only queries whose count overflowed
+  if (a.gate != nullptr && (int64_t)a.gate[(size_t)qi * kCountStride] <= a.gate_cap) return;
   const float* qg = a.q + (size_t)qi * a.d;
   for (int i = threadIdx.x; i < qfl; i += 256) {
     float v = i < a.d ? qg[i] : 0.f;
@@ -838,8 +840,7 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   p->smem_dma = 0;
   if (dtype == FX_DTYPE_QU8 && W == 16 && nch == 1 && U % FX_Q8DMA_U == 0) {
     const size_t sd = smem + (size_t)4 * FX_Q8DMA_STAGES * FX_Q8DMA_U * L * 1024;
-    const char* env = getenv("FX_Q8_DMA");
-    if (sd <= 80 * 1024 && (env == nullptr || atoi(env) != 0)) {  // >= 2 workgroups per CU
+    if (sd <= 80 * 1024 && option(kOptQ8Dma) != 0) {  // >= 2 workgroups per CU
       p->fn_dma = select_q8_dma_kernel(metric, L);
       p->smem_dma = sd;
     }
@@ -866,11 +867,11 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   }
   // Two 256-thread blocks per CU already saturate HBM with the pipelined
   // tiles (sweep in profiles/), and fewer blocks mean fewer candidate lists
-  // to merge.  FX_SCAN_BLOCKS_PER_CU overrides (tuning knob, microbench).
+  // to merge.  FX_SCAN_BLOCKS_PER_CU overrides (diagnostic builds, microbench).
   // Rows of >= 12 slots per lane (768-d f32, 1536-d f16 and longer): one
   // block per CU reads as fast or faster (1536-d f16: 4.50 vs 4.66 ms).
-  int cap_occ = dtype == FX_DTYPE_QU8 ? 3 : L >= 12 ? 1 : 2;
-  if (const char* env = getenv("FX_SCAN_BLOCKS_PER_CU")) cap_occ = atoi(env);
+  const int cap_occ =
+      diag_env("FX_SCAN_BLOCKS_PER_CU", dtype == FX_DTYPE_QU8 ? 3 : L >= 12 ? 1 : 2);
   if (cap_occ > 0 && cap_occ < occ) occ = cap_occ;
   if (occ < 1) occ = 1;
   const int64_t max_blocks = (int64_t)cus * occ;
@@ -891,14 +892,13 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   p->nlists = blocks;  // one list per block (the epilogue folds its 4 waves)
   // Block steps dealt round-robin over the grid for rows of >= 1 KB, each
   // block one contiguous range below that (sweep over d and dtype:
-  // profiles/r02_scan_interleave_sweep.log).  FX_SCAN_INTERLEAVE overrides.
+  // profiles/r02_scan_interleave_sweep.log).  The "scan_interleave" option
+  // (test switch) overrides.
   const int esize = dtype == FX_DTYPE_F32 ? 4 : dtype == FX_DTYPE_F16 ? 2 : 1;
   p->interleave = kInterleaveDefault && d * esize >= 1024;
-  if (const char* env = getenv("FX_SCAN_INTERLEAVE")) p->interleave = atoi(env) != 0;
-  // FX_SCAN_PIPE=0: one register tile per wave in flight (tuning knob)
-  if (const char* env = getenv("FX_SCAN_PIPE")) {
-    if (atoi(env) == 0) p->interleave |= 2;
-  }
+  if (option(kOptScanInterleave) >= 0) p->interleave = option(kOptScanInterleave) != 0;
+  // FX_SCAN_PIPE=0: one register tile per wave in flight (diagnostic builds)
+  if (diag_env("FX_SCAN_PIPE", 1) == 0) p->interleave |= 2;
   return FX_OK;
 }
 

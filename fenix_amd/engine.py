@@ -21,6 +21,7 @@ import ctypes
 import os
 import threading
 import weakref
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -212,11 +213,119 @@ def stage_sharded(col: pa.ChunkedArray, devs: Sequence[torch.device]) -> List[Pi
     return pieces
 
 
-class CorpusCache:
-    """HBM-resident embedding columns keyed by (path, file version, column, devices)."""
+def _budget_bytes(dev: int) -> int:
+    """HBM the resident caches may hold on device ``dev``.
+
+    ``FENIX_AMD_HBM_BUDGET``: bytes (an integer), or a fraction of the device's
+    memory (a number <= 1); default 0.85 of it, the rest left to workspaces,
+    query batches and the caller's own tensors."""
+    env = os.environ.get("FENIX_AMD_HBM_BUDGET", "").strip()
+    total = torch.cuda.get_device_properties(dev).total_memory
+    if env:
+        v = float(env)
+        return int(v * total) if v <= 1.0 else int(v)
+    return int(0.85 * total)
+
+
+class Residency:
+    """LRU accounting of the HBM held by the resident caches: staged corpus
+    shards (``CorpusCache``) and filter images (``Engine.filter_image``).
+
+    The reference holds nothing between calls (it re-maps the Arrow file per
+    search, src/fenix/io/index/index.py:97); a server keeping tables resident
+    must bound them.  Before a cache allocates, ``reserve`` evicts least-
+    recently-used entries until the new bytes fit the device's budget:
+    filter images first (rebuilt in ~10 ms, and a search is correct without
+    one), then corpus entries (restaged from the Arrow file on their next
+    search).  An entry in use by a running search keeps its tensors alive
+    through that search's own references; eviction only drops the cache's."""
+
+    IMAGE, CORPUS = 0, 1
 
     def __init__(self) -> None:
-        self._lock = threading.Lock()
+        self._lock = threading.RLock()
+        # key -> (kind, {device index: bytes}, evict callback); order = LRU first
+        self._items: "OrderedDict[tuple, tuple]" = OrderedDict()
+        self.evictions = 0
+
+    def used(self, dev: int) -> int:
+        with self._lock:
+            return sum(b.get(dev, 0) for _, b, _ in self._items.values())
+
+    def add(self, key: tuple, kind: int, nbytes: Dict[int, int], evict) -> None:
+        with self._lock:
+            self._items[key] = (kind, dict(nbytes), evict)
+            self._items.move_to_end(key)
+
+    def touch(self, key: tuple) -> None:
+        with self._lock:
+            if key in self._items:
+                self._items.move_to_end(key)
+
+    def remove(self, key: tuple) -> None:
+        with self._lock:
+            self._items.pop(key, None)
+
+    def reserve(self, need: Dict[int, int], keep: Sequence[tuple] = ()) -> bool:
+        """Evict until ``need`` more bytes fit every listed device's budget;
+        False when they cannot (everything evictable is gone).  The victims'
+        callbacks run after this object's lock is released (they take their
+        cache's lock)."""
+        victims = []
+        ok = True
+        with self._lock:
+            for dev, extra in need.items():
+                budget = _budget_bytes(dev)
+                used = self.used(dev)
+                for kind in (self.IMAGE, self.CORPUS):
+                    for key in [k for k, v in self._items.items()
+                                if v[0] == kind and v[1].get(dev, 0) > 0 and k not in keep]:
+                        if used + extra <= budget:
+                            break
+                        item = self._items.pop(key)
+                        used -= item[1].get(dev, 0)
+                        victims.append(item)
+                ok = ok and used + extra <= budget
+        for item in victims:
+            self.evictions += 1
+            item[2]()
+        return ok
+
+    def evict(self, key: tuple) -> None:
+        with self._lock:
+            item = self._items.pop(key, None)
+        if item is not None:
+            self.evictions += 1
+            item[2]()
+
+    def evict_all(self, kind: Optional[int] = None) -> None:
+        with self._lock:
+            keys = [k for k, v in self._items.items() if kind is None or v[0] == kind]
+        for k in keys:
+            self.evict(k)
+
+
+RESIDENT = Residency()
+
+
+def _with_oom_retry(fn):
+    """Run ``fn``; on a device out-of-memory error evict every cached image and
+    corpus once, release torch's cached blocks and run it again."""
+    try:
+        return fn()
+    except torch.cuda.OutOfMemoryError:
+        RESIDENT.evict_all()
+        torch.cuda.empty_cache()
+        return fn()
+
+
+class CorpusCache:
+    """HBM-resident embedding columns keyed by (path, file version, column,
+    devices), within the devices' HBM budgets (``Residency``)."""
+
+    def __init__(self) -> None:
+        # re-entrant: staging may evict this cache's own older entries
+        self._lock = threading.RLock()
         self._entries: Dict[tuple, _Entry] = {}
 
     @staticmethod
@@ -228,20 +337,50 @@ class CorpusCache:
     def get(self, path: str, table: pa.Table, column: str,
             devs: Sequence[torch.device]) -> _Entry:
         key = self._key(path, column, devs)
+        rkey = ("corpus", id(self)) + key
         with self._lock:
             hit = self._entries.get(key)
             if hit is not None:
+                RESIDENT.touch(rkey)
                 return hit
             # drop stale versions of the same file/column/devices
             for k in [k for k in self._entries if k[0] == key[0] and k[2:] == key[2:]]:
-                del self._entries[k]
-            entry = _Entry(key, table, stage_sharded(table.column(column), devs))
+                self._drop(k)
+            col = table.column(column)
+            need = self._bytes(col, devs)
+            RESIDENT.reserve(need)
+            entry = _Entry(key, table, _with_oom_retry(lambda: stage_sharded(col, devs)))
             self._entries[key] = entry
+            RESIDENT.add(rkey, Residency.CORPUS, need, lambda: self._evicted(key))
             return entry
+
+    @staticmethod
+    def _bytes(col: pa.ChunkedArray, devs: Sequence[torch.device]) -> Dict[int, int]:
+        from .distributed import shard_rows
+
+        _, _, ndt = value_dtype(col.type)
+        row = list_size(col.type) * ndt.itemsize
+        need: Dict[int, int] = {}
+        for i, dev in enumerate(devs):
+            _, count = shard_rows(len(col), len(devs), i)
+            need[dev.index] = need.get(dev.index, 0) + count * row
+        return need
+
+    def _evicted(self, key: tuple) -> None:
+        with self._lock:
+            self._entries.pop(key, None)
+
+    def _drop(self, key: tuple) -> None:
+        self._entries.pop(key, None)
+        RESIDENT.remove(("corpus", id(self)) + key)
+
+    def __contains__(self, key: tuple) -> bool:
+        return key in self._entries
 
     def clear(self) -> None:
         with self._lock:
-            self._entries.clear()
+            for k in list(self._entries):
+                self._drop(k)
 
 
 CACHE = CorpusCache()
@@ -288,11 +427,22 @@ class Engine:
                      metric: int) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
         """The fp16 filter image (+ row sums of squares) of an f32 shard for a
         search that runs the batched filter (fx_filter_image_used), built on
-        first use and kept while the corpus tensor lives and is unmodified
-        (its data pointer, shape and torch version counter); (None, None) when
-        the search does not read one, when ``FENIX_AMD_FILTER_IMAGE=0``, or
-        when free HBM cannot hold it.  Results never depend on it: the filter
-        only selects candidates, which are rescored from the f32 rows."""
+        first use and kept while the corpus tensor lives and is unmodified;
+        (None, None) when the search does not read one, when
+        ``FENIX_AMD_FILTER_IMAGE=0``, or when the HBM budget (``Residency``)
+        cannot hold it.  The filter only selects candidates, which are
+        rescored from the f32 rows, so results never depend on whether an
+        image is used.
+
+        Invariant: an image is valid only while its corpus is unchanged.
+        Staleness is detected through the tensor's identity, data pointer,
+        shape and torch version counter, which every torch write and
+        ``Engine.fill`` bump; a writer that bypasses torch (a raw pointer
+        through ctypes, DLPack, another library) must call
+        ``invalidate_image`` afterwards.
+
+        The image is built on the caller's current stream; a search on another
+        stream waits for the build through an event recorded after it."""
         if (shard.dtype_id != _lib.DTYPE_F32
                 or os.environ.get("FENIX_AMD_FILTER_IMAGE", "1") == "0"
                 or not _lib.filter_image_used(shard.n, shard.d, shard.dtype_id, nq, k, metric)):
@@ -303,27 +453,52 @@ class Engine:
         if not t.is_contiguous() or t.data_ptr() % 16 != 0:
             return None, None
         key = id(t)
-        # (the layout, FX_IMAGE_TILED, is read by the library at build and at search)
-        sig = (t.data_ptr(), tuple(t.shape), t._version,
-               os.environ.get("FX_IMAGE_TILED", "1") != "0")
+        rkey = ("image", self.device.index, key)
+        sig = (t.data_ptr(), tuple(t.shape), t._version)
         hit = self._images.get(key)
         if hit is not None and hit[0] == sig:
+            RESIDENT.touch(rkey)
+            torch.cuda.current_stream(self.device).wait_event(hit[3])
             return hit[1], hit[2]
-        self._images.pop(key, None)  # a stale image: free it before building the new one
+        self.invalidate_image(t)  # a stale image: free it before building the new one
         n, d = shard.n, shard.d
         ib, rb = ctypes.c_size_t(0), ctypes.c_size_t(0)
         _lib.check(_lib.load().fx_filter_image_bytes(n, d, ctypes.byref(ib), ctypes.byref(rb)))
         need = ib.value + rb.value
-        free, _ = torch.cuda.mem_get_info(self.device)
-        if need + (1 << 30) > free:
+        if not RESIDENT.reserve({self.device.index: need}):
             return None, None
-        img = torch.empty((ib.value // 2,), dtype=torch.float16, device=self.device)
-        info = torch.empty((n,), dtype=torch.float32, device=self.device)
+        free, _ = torch.cuda.mem_get_info(self.device)
+        cached = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
+        if need + (1 << 30) > free + cached:
+            return None, None
+        try:
+            img = torch.empty((ib.value // 2,), dtype=torch.float16, device=self.device)
+            info = torch.empty((n,), dtype=torch.float32, device=self.device)
+        except torch.cuda.OutOfMemoryError:
+            return None, None  # the f32 filter (no image) is always correct
         _lib.check(_lib.load().fx_filter_image(_ptr(t), n, d, _ptr(img), _ptr(info),
                                                self._stream()))
-        self._images[key] = (sig, img, info)
-        weakref.finalize(t, self._images.pop, key, None)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._images[key] = (sig, img, info, ev)
+        RESIDENT.add(rkey, Residency.IMAGE, {self.device.index: need},
+                     lambda: self._images.pop(key, None))
+        weakref.finalize(t, self._drop_image, key)
         return img, info
+
+    def clear_images(self) -> None:
+        """Drop every filter image this engine holds."""
+        for key in list(self._images):
+            self._drop_image(key)
+
+    def invalidate_image(self, t: torch.Tensor) -> None:
+        """Drop the filter image of corpus tensor ``t`` (for writers that
+        modify it behind torch's version counter)."""
+        self._drop_image(id(t))
+
+    def _drop_image(self, key: int) -> None:
+        self._images.pop(key, None)
+        RESIDENT.remove(("image", self.device.index, key))
 
     def search_shard(self, shard: Shard, queries: torch.Tensor, metric: int, k: int,
                      mask: Optional[torch.Tensor], out_dist: torch.Tensor,
@@ -621,11 +796,14 @@ def _search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: 
                 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Exact top-k over shards that may live on several devices.
 
-    Each device's shards are searched by that device's Engine (all launches are
-    asynchronous, so the devices scan concurrently); the per-device [nq, k]
-    results are copied to the first device (peer-to-peer over xGMI, a few KB)
-    and merged there by fx_topk_merge.  Single process: the gather is a copy,
-    not a collective (the one-process-per-GPU path uses RCCL, distributed.py).
+    Each device's shards are searched by that device's Engine.  No library
+    call waits for the host (the batched path's overflow fallback is gated on
+    the device, fx_knn_reduce), so this loop queues every device's scan and
+    merge back to back and the devices scan concurrently; the per-device
+    [nq, k] results are copied to the first device (peer-to-peer over xGMI, a
+    few KB) and merged there by fx_topk_merge.  Single process: the gather is
+    a copy, not a collective (the one-process-per-GPU path uses RCCL,
+    distributed.py).
     """
     groups: Dict[torch.device, List[int]] = {}
     for i, s in enumerate(shards):

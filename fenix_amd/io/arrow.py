@@ -26,8 +26,11 @@ def file_version(path: str) -> tuple:
     a file's contents (mmap'd tables, HBM shards, codings) is stamped with.
     ``make`` replaces files atomically (new inode) and bumps the generation,
     so a rewrite with the same size inside one mtime tick is still seen."""
-    st = os.stat(path)
+    # stat and generation read under the lock ``replace`` holds across the
+    # rename and the bump: a reader never pairs the new file with the old
+    # generation (which would restage the corpus once more after the bump)
     with _gen_lock:
+        st = os.stat(path)
         gen = _GEN.get(os.path.abspath(path), 0)
     return (st.st_size, st.st_mtime_ns, st.st_ino, gen)
 
@@ -67,7 +70,7 @@ def temp_path(path: str) -> str:
 
 def replace(tmp: str, path: str) -> None:
     """Rename a fully written ``tmp`` over ``path`` and bump its generation."""
-    os.replace(tmp, path)
     with _gen_lock:
+        os.replace(tmp, path)
         key = os.path.abspath(path)
         _GEN[key] = _GEN.get(key, 0) + 1

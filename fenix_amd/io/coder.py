@@ -208,8 +208,13 @@ def make(root: str, name: str, source: str | Sequence[str], column: str, config:
     path = _path(root, name)
     os.makedirs(os.path.dirname(path), exist_ok=True)
     tmp = arrow.temp_path(path)
-    with open(tmp, "wb") as f:
-        torch.save({"tensor": tensor, "column": _type_bytes(vtype), "config": dict(config)}, f)
+    try:
+        with open(tmp, "wb") as f:
+            torch.save({"tensor": tensor, "column": _type_bytes(vtype), "config": dict(config)}, f)
+    except BaseException:
+        if os.path.exists(tmp):
+            os.remove(tmp)
+        raise
     arrow.replace(tmp, path)
     return load(root, name)
 

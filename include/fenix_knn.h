@@ -67,6 +67,37 @@ const char* fx_last_error(void);
 /* Number of visible HIP devices. */
 int fx_device_count(int* out);
 
+/*
+ * Process-wide options, set explicitly by the host.  The library reads no
+ * environment variable: a serving process's kernel selection cannot change
+ * through its environment.  Name, default, meaning:
+ *   "batched"             1  0: each query of a batch runs the single-query scan
+ *   "batch_min_queries"   2  smallest batch that takes the batched filter (1:
+ *                            single float32 queries too, with a filter image)
+ * Test switches (they change which code runs, never the results):
+ *   "batch_cap"           0  candidate buffer per query of the batched filter
+ *                            (0: max(64 k, 16 K); smaller than 16 k is ignored)
+ *   "batch_sample_ratio"  0  row-sample ratio of the filter phases (0: cap / 4k;
+ *                            only denser samples are accepted)
+ *   "force_fallback"      0  1: every batched query is recomputed by the exact
+ *                            single-query scan, as if its candidates overflowed
+ *   "scan_interleave"    -1  -1: by row size; 0: one row range per workgroup;
+ *                            1: block steps dealt round-robin over the grid
+ *   "q8_dma"              1  0: quint8 scans without the LDS-DMA ring
+ * fx_set_option: FX_EINVAL for an unknown name.  Options are read when a call
+ * plans its launches; set them while no search is in flight.
+ */
+int fx_set_option(const char* name, int64_t value);
+int fx_get_option(const char* name, int64_t* out);
+
+/*
+ * Host-blocking synchronisations (stream / device synchronise, blocking copy)
+ * the library has performed since it was loaded.  Every entry point is
+ * asynchronous on its stream, so searches leave this count unchanged; tests
+ * assert that, e.g. across a search over shards on several devices.
+ */
+uint64_t fx_host_sync_count(void);
+
 /* Largest k of the fused scan + merge path (1024).  Any larger k (the
  * reference's maxval is unbounded, index.py:165-168) is served by a
  * distance-mode scan + radix sort of all n composites (knn_large.hip): every
@@ -108,9 +139,12 @@ int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
  * with d % 8 == 0, 16-B aligned corpus, any metric) take the matrix-core
  * path: fx_knn_scan runs the sampled-threshold phases of the fp16-MFMA bound
  * filter and rescores the surviving candidates exactly, so the results are
- * bit-identical to the single-query scan; fx_knn_reduce synchronises the
- * stream once to recompute any query whose candidates overflowed (exact
- * single-query scan), so it is not graph-capturable.
+ * bit-identical to the single-query scan; fx_knn_reduce recomputes any
+ * query whose candidates overflowed with the exact single-query scan, decided
+ * on the device: the fallback launches read the per-query candidate counts
+ * and their workgroups return at once for queries that did not overflow, so
+ * no call synchronises with the host and the whole search can be queued on
+ * several devices back to back (or captured in a graph).
  */
 int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
                 const float* queries, int64_t nq, int metric, int64_t k,

@@ -316,3 +316,122 @@ int fx_ref_distances(const void* x, int dtype, int64_t n, int64_t d, const float
   }
   return 0;
 }
+
+/* Round-to-nearest-even float -> half bits (the device's __float2half / the
+ * fp16 corpus cast, torch .half()); used by fx_ref_knn_gen for fp16 corpora. */
+static uint16_t float_to_half(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  const uint32_t sign = (u >> 16) & 0x8000u;
+  uint32_t a = u & 0x7fffffffu;
+  if (a >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (a > 0x7f800000u ? 0x200u : 0u));
+  if (a >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u); /* rounds to >= 65520: inf */
+  if (a < 0x38800000u) {                                     /* subnormal or zero half */
+    if (a < 0x33000000u) return (uint16_t)sign;              /* < 2^-25: rounds to 0 */
+    const uint32_t m = (a & 0x7fffffu) | 0x800000u;
+    const int sh = 126 - (int)(a >> 23); /* 14..24 */
+    uint32_t h = m >> (sh);
+    const uint32_t rem = m & ((1u << sh) - 1u), half = 1u << (sh - 1);
+    if (rem > half || (rem == half && (h & 1u))) ++h;
+    return (uint16_t)(sign | h);
+  }
+  uint32_t h = ((a >> 23) - 112u) << 10 | ((a >> 13) & 0x3ffu);
+  const uint32_t rem = a & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+  return (uint16_t)(sign | h);
+}
+
+/*
+ * Top-k over a corpus GENERATED on the fly: row r is fx_ref_fill's row
+ * (seed, row_base + r, cluster), rounded to fp16 when as_f16 (the fp16
+ * corpora of the tests), except the n_over rows listed in over_rows (local
+ * rows, ascending or not), whose values are over_vals[i][d] (f32, or the f32
+ * value of an fp16 element).  Corpora of 80M x 768 (configs[3], 246 GB) or
+ * 50M x 1536 (configs[4]) are checked this way without holding them in host
+ * memory.  Same arithmetic, ordering and outputs as fx_ref_knn.
+ */
+int fx_ref_knn_gen(uint64_t seed, int64_t row_base, int64_t n, int64_t d, int64_t cluster,
+                   int as_f16, const int64_t* over_rows, const float* over_vals, int64_t n_over,
+                   const float* q, int64_t nq, int metric, int64_t k, int precision, int threads,
+                   double* out_dist, int64_t* out_row) {
+  if (n < 0 || d < 1 || nq < 0 || k < 1 || metric < 0 || metric > 2) return -1;
+#ifdef _OPENMP
+  int nt = threads > 0 ? threads : omp_get_max_threads();
+#else
+  int nt = 1;
+  (void)threads;
+#endif
+  const int64_t chunk = 1024; /* rows generated per block */
+  cand_t* heaps = (cand_t*)malloc(sizeof(cand_t) * (size_t)k * (size_t)nt * (size_t)nq);
+  int64_t* sizes = (int64_t*)calloc((size_t)nt * (size_t)nq, sizeof(int64_t));
+  cand_t* all = (cand_t*)malloc(sizeof(cand_t) * (size_t)k * (size_t)nt);
+  double* qn64 = (double*)malloc(sizeof(double) * (size_t)(nq > 0 ? nq : 1));
+  float* qn32 = (float*)malloc(sizeof(float) * (size_t)(nq > 0 ? nq : 1));
+  if (!heaps || !sizes || !all || !qn64 || !qn32) {
+    free(heaps); free(sizes); free(all); free(qn64); free(qn32);
+    return -1;
+  }
+  for (int64_t qi = 0; qi < nq; ++qi) {
+    const float* qv = q + qi * d;
+    double s = 0.0;
+    for (int64_t c = 0; c < d; ++c) s += (double)qv[c] * (double)qv[c];
+    s = sqrt(s);
+    qn64[qi] = s < 1e-12 ? 1e-12 : s;
+    float a[8] = {0}, s32 = 0.f;
+    int64_t c = 0;
+    for (; c + 8 <= d; c += 8)
+      for (int j = 0; j < 8; ++j) a[j] += qv[c + j] * qv[c + j];
+    for (int j = 0; j < 8; ++j) s32 += a[j];
+    for (; c < d; ++c) s32 += qv[c] * qv[c];
+    s32 = sqrtf(s32);
+    qn32[qi] = s32 < 1e-12f ? 1e-12f : s32;
+  }
+  const int64_t nblk = (n + chunk - 1) / chunk;
+#pragma omp parallel num_threads(nt)
+  {
+#ifdef _OPENMP
+    int tid = omp_get_thread_num();
+#else
+    int tid = 0;
+#endif
+    float* rows = (float*)malloc(sizeof(float) * (size_t)chunk * (size_t)d);
+#pragma omp for schedule(dynamic, 4)
+    for (int64_t b = 0; b < nblk; ++b) {
+      const int64_t r0 = b * chunk, m = (n - r0) < chunk ? (n - r0) : chunk;
+      fx_ref_fill(rows, m, d, seed, row_base + r0, cluster);
+      for (int64_t i = 0; i < n_over; ++i) {
+        if (over_rows[i] >= r0 && over_rows[i] < r0 + m)
+          memcpy(rows + (over_rows[i] - r0) * d, over_vals + i * d, sizeof(float) * (size_t)d);
+      }
+      if (as_f16) {
+        for (int64_t e = 0; e < m * d; ++e) rows[e] = half_to_float(float_to_half(rows[e]));
+      }
+      for (int64_t qi = 0; qi < nq; ++qi) {
+        cand_t* h = heaps + ((size_t)qi * nt + tid) * k;
+        int64_t hs = sizes[(size_t)qi * nt + tid];
+        for (int64_t r = 0; r < m; ++r) {
+          cand_t c;
+          c.d = precision == 32 ? row_dist32(rows + r * d, NULL, q + qi * d, d, metric, qn32[qi])
+                                : row_dist64(rows + r * d, NULL, q + qi * d, d, metric, qn64[qi]);
+          c.r = row_base + r0 + r;
+          heap_push(h, &hs, k, c);
+        }
+        sizes[(size_t)qi * nt + tid] = hs;
+      }
+    }
+    free(rows);
+  }
+  for (int64_t qi = 0; qi < nq; ++qi) {
+    int64_t m = 0;
+    for (int t = 0; t < nt; ++t)
+      for (int64_t i = 0; i < sizes[(size_t)qi * nt + t]; ++i)
+        all[m++] = heaps[((size_t)qi * nt + t) * k + i];
+    qsort(all, (size_t)m, sizeof(cand_t), cmp_cand);
+    for (int64_t i = 0; i < k; ++i) {
+      out_dist[qi * k + i] = i < m ? all[i].d : NAN;
+      out_row[qi * k + i] = i < m ? all[i].r : -1;
+    }
+  }
+  free(heaps); free(sizes); free(all); free(qn64); free(qn32);
+  return 0;
+}

@@ -168,6 +168,9 @@ def lib() -> ctypes.CDLL:
         L.fx_ref_distances.argtypes = [vp, ctypes.c_int, i64, i64, vp, i64, ctypes.c_int,
                                        ctypes.c_int, vp]
         L.fx_ref_distances.restype = ctypes.c_int
+        L.fx_ref_knn_gen.argtypes = [u64, i64, i64, i64, i64, ctypes.c_int, vp, vp, i64, vp, i64,
+                                     ctypes.c_int, i64, ctypes.c_int, ctypes.c_int, vp, vp]
+        L.fx_ref_knn_gen.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -220,6 +223,41 @@ def knn(
                           _ptr(bm), precision, threads, _ptr(od), _ptr(orow))
     if rc != 0:
         raise ValueError("fx_ref_knn failed")
+    return od, orow
+
+
+def knn_gen(
+    n: int,
+    d: int,
+    seed: int,
+    q: np.ndarray,
+    metric: str,
+    k: int,
+    row_base: int = 0,
+    cluster: int = 0,
+    dtype=np.float32,
+    overrides: Optional[dict] = None,
+    precision: int = 64,
+    threads: int = 0,
+) -> Tuple[np.ndarray, np.ndarray]:
+    """:func:`knn` over ``fill_normal(n, d, seed, row_base, cluster, dtype)``
+    generated block by block in C (never materialised: the full-size
+    configs[3]/[4] corpora are 246 / 154 GB).  ``overrides``: {local row:
+    [d] values} replacing generated rows (planted neighbours), cast to
+    ``dtype`` like the generated ones."""
+    q = np.ascontiguousarray(np.atleast_2d(q), dtype=np.float32)
+    items = sorted((overrides or {}).items())
+    rows = np.array([r for r, _ in items], dtype=np.int64)
+    vals = np.ascontiguousarray(np.array([np.asarray(v, dtype=np.float32) for _, v in items],
+                                         dtype=np.float32).reshape(len(items), d))
+    nq = q.shape[0]
+    od = np.empty((nq, k), dtype=np.float64)
+    orow = np.empty((nq, k), dtype=np.int64)
+    rc = lib().fx_ref_knn_gen(seed, row_base, n, d, cluster, int(np.dtype(dtype) == np.float16),
+                              _ptr(rows), _ptr(vals), len(items), _ptr(q), nq,
+                              METRIC_IDS[metric], k, precision, threads, _ptr(od), _ptr(orow))
+    if rc != 0:
+        raise ValueError("fx_ref_knn_gen failed")
     return od, orow
 
 

@@ -33,9 +33,10 @@ def scale_of(x: np.ndarray, q: np.ndarray, metric: str) -> np.ndarray:
     return np.maximum(qn + xn, 1e-30)
 
 
-def check_topk(gd, gr, od, orow, x, q, metric, allow_near_ties=True):
+def check_topk(gd, gr, od, orow, x, q, metric, allow_near_ties=True, details=None):
     """Return the number of near-tie positions used; raise AssertionError on a
-    real mismatch."""
+    real mismatch.  ``details`` (a list): receives one dict per near-tie
+    position (query, position, GPU row, oracle row, their float64 distances)."""
     gd = np.asarray(gd, dtype=np.float64)
     od = np.asarray(od, dtype=np.float64)
     gr = np.asarray(gr)
@@ -83,10 +84,16 @@ def check_topk(gd, gr, od, orow, x, q, metric, allow_near_ties=True):
                     f"query {i} pos {j}: row {r} belongs at {jj} "
                     f"(d64 {od[i, jj]!r} vs {od[i, j]!r})"
                 )
+                d64_gpu_row = float(od[i, jj])
             else:
                 # boundary near-tie: row r must be as close as the last kept one
                 assert abs(gd[i, j] - od[i, nv - 1]) <= near + DIST_RTOL * abs(od[i, nv - 1]), (
                     f"query {i} pos {j}: row {r} not in oracle top-k"
                 )
+                d64_gpu_row = None  # outside the oracle's top-k: its f64 distance is not at hand
             near_used += 1
+            if details is not None:
+                details.append({"query": i, "pos": int(j), "gpu_row": r, "oracle_row": int(o[j]),
+                                "gpu_f32_dist": float(gd[i, j]), "gpu_row_d64": d64_gpu_row,
+                                "oracle_row_d64": float(od[i, j]), "near_tol": near})
     return near_used

@@ -17,7 +17,7 @@ HEADER = os.path.join(ROOT, "include", "fenix_knn.h")
 
 def declared_symbols():
     text = open(HEADER).read()
-    return set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(fx_\w+)\s*\(", text, re.M))
+    return set(re.findall(r"^\s*(?:int|int64_t|uint64_t|const char\*)\s+(fx_\w+)\s*\(", text, re.M))
 
 
 def test_header_and_binding_agree():
@@ -40,8 +40,31 @@ def test_library_is_gfx950():
 
 def test_version_and_limits():
     lib = _lib.load()
-    assert lib.fx_version() == 101  # 1.1: coded index, row lists, _ex, large k, RCCL
+    assert lib.fx_version() == 102  # 1.2: options, device-gated overflow fallback
     assert _lib.max_k() == 1024
+
+
+def test_options_round_trip_and_unknown_names():
+    for name in _lib.OPTIONS:
+        old = _lib.get_option(name)
+        with _lib.options(**{name: old + 3}):
+            assert _lib.get_option(name) == old + 3
+        assert _lib.get_option(name) == old
+    assert _lib.get_option("batched") == 1 and _lib.get_option("batch_min_queries") == 2
+    with pytest.raises(ValueError, match="unknown option"):
+        _lib.set_option("no_such_option", 1)
+
+
+def test_product_library_reads_no_environment_switches():
+    """Kernel selection is not reachable through the environment: the
+    rejected variants and tuning knobs exist only in `make diag` builds.
+    (rocPRIM, linked for the radix sorts, reads its own debug variables.)"""
+    data = open(_lib.LIB_PATH, "rb").read()
+    for name in (b"FX_BATCH", b"FX_FILTER_RING", b"FX_IMAGE_TILED", b"FX_FILTER_DIAG",
+                 b"FX_SCAN_INTERLEAVE", b"FX_SCAN_PIPE", b"FX_SCAN_BLOCKS_PER_CU",
+                 b"FX_MERGE_GROUP", b"FX_Q8_DMA"):
+        assert name not in data, name
+    assert _lib.host_sync_count() == 0
 
 
 def test_invalid_arguments_are_rejected_before_any_device_work():

@@ -19,9 +19,9 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
         "roofline", "cpu_baseline"}
 
 
-def run_bench(*args: str) -> dict:
+def run_bench(*args: str, env=None) -> dict:
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args],
-                         capture_output=True, text=True, timeout=300, cwd=ROOT)
+                         capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout
@@ -69,3 +69,25 @@ def test_bench_rccl_path_one_rank():
     rec = json.loads(lines[0])
     assert rec["config"]["parallelism"] == "row-shard x1 + RCCL all-gather"
     assert rec["n_gpus"] == 1 and rec["value"] > 0
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` without a launcher starts 2 ranks itself (here
+    with gloo, two ranks sharing the one GPU of the box: RCCL refuses a
+    duplicate device) and reports n_gpus 2 over 2 x rows."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    rec = run_bench("--gpus", "2", "--dist-backend", "gloo", "--rows", "200000", "--steps", "3",
+                    "--warmup", "1", "--no-cpu-baseline", env=env)
+    assert rec["n_gpus"] == 2
+    assert rec["config"]["total_rows"] == 400000
+    assert rec["config"]["parallelism"] == "row-shard x2 + gloo all-gather"
+
+
+def test_bench_gpus_must_match_world_size():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--rows", "100000", "--steps", "1", "--no-cpu-baseline"],
+                         capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert out.returncode != 0
+    assert "WORLD_SIZE=1" in out.stderr

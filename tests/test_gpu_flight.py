@@ -268,6 +268,34 @@ def test_empty_source(env):
     np.testing.assert_array_equal(both.column("id").to_numpy(), orow[0])
 
 
+def test_hbm_budget_evicts_and_restages(env, monkeypatch):
+    """With an HBM budget below two staged columns (FENIX_AMD_HBM_BUDGET), the
+    second table's staging evicts the first (least recently used); the first
+    is restaged on its next search, with identical results."""
+    from fenix_amd import engine
+
+    root = env["root"]
+    x2 = O.fill_normal(NUM_VECTORS, VECTOR_SIZE, seed=91)
+    env["flight"].make_table("test/table2", pa.Table.from_batches(batches(x2), SCHEMA).to_reader())
+    t = O.fill_normal(1, VECTOR_SIZE, seed=92)[0]
+    engine.CACHE.clear()
+    engine.RESIDENT.evict_all(engine.Residency.IMAGE)  # images of earlier tests' corpora
+    first = index.call(root, None, "test/table", "vector", target=t, metric="l2", maxval=50)
+    col_bytes = NUM_VECTORS * VECTOR_SIZE * 4
+    monkeypatch.setenv("FENIX_AMD_HBM_BUDGET", str(int(1.5 * col_bytes)))
+    ev0 = engine.RESIDENT.evictions
+    other = index.call(root, None, "test/table2", "vector", target=t, metric="l2", maxval=50)
+    assert engine.RESIDENT.evictions == ev0 + 1
+    assert engine.RESIDENT.used(0) <= 1.5 * col_bytes
+    od, orow = O.knn(x2, t[None], "l2", 50)
+    np.testing.assert_array_equal(other.column("id").to_numpy(), orow[0])
+    again = index.call(root, None, "test/table", "vector", target=t, metric="l2", maxval=50)
+    assert engine.RESIDENT.evictions == ev0 + 2  # table2 made room for table's restaging
+    assert again.equals(first)
+    monkeypatch.delenv("FENIX_AMD_HBM_BUDGET")
+    engine.CACHE.clear()
+
+
 def test_remove(env):
     flight = env["flight"]
     flight.remove()

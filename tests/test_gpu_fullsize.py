@@ -8,6 +8,9 @@ shards (the multi-GPU merge identity) and a planted nearest neighbour."""
 
 from __future__ import annotations
 
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -18,6 +21,21 @@ from oracle import oracle as O
 from tests.parity import check_topk
 
 pytestmark = pytest.mark.gpu
+
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+
+
+def record_near_ties(case, count, details):
+    """Append a case's near-tie count and positions to gpurun_out/near_ties.json."""
+    os.makedirs(OUT, exist_ok=True)
+    path = os.path.join(OUT, "near_ties.json")
+    rec = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            rec = json.load(f)
+    rec[case] = {"near_ties": count, "positions": details}
+    with open(path, "w") as f:
+        json.dump(rec, f, indent=1)
 
 N, D, K = 10_000_000, 768, 100
 
@@ -50,8 +68,15 @@ def test_full_corpus_vs_oracle(big, metric, batched):
         gd, gr = torch.cat([d for d, _ in res]), torch.cat([r for _, r in res])
     gd, gr = gd.cpu().numpy(), gr.cpu().numpy()
     od, orow = O.knn(host, q, metric, K)
-    near = check_topk(gd, gr, od, orow, host[:100_000], q, metric)
-    assert near <= 4, f"{near} near-tie positions"
+    details = []
+    near = check_topk(gd, gr, od, orow, host[:100_000], q, metric, details=details)
+    # the count is reported (and each position recorded with its float64
+    # distances) so a run shows whether the ids were bit-exact
+    print(f"near-ties {metric} batched={batched}: {near}")
+    record_near_ties(f"configs[1]_{metric}_{'batched' if batched else 'single'}", near, details)
+    # measured 0 for every metric, single and batched (gpurun_out/near_ties.json,
+    # profiles/r03_near_ties.json): the ids are bit-exact at full size
+    assert near == 0, f"{near} near-tie positions: {details}"
 
 
 @pytest.mark.parametrize("metric", ["l2", "cosine", "inner_product"])

@@ -355,9 +355,10 @@ def test_batched_masked_and_clustered(eng):
         check_topk(gd, gr, od, orow, xh, q, metric)
 
 
-def test_batched_overflow_fallback(eng, monkeypatch):
+def test_batched_overflow_fallback(eng):
     """Queries whose final candidates overflow are recomputed by the exact
-    single-query scan: forced for every query, results must not change."""
+    single-query scan (gated on the device): forced for every query, results
+    must not change."""
     n, d, nq, k = 40_000, 128, 16, 20
     x = gpu_fill(eng, n, d, seed=9)
     xh = O.fill_normal(n, d, 9)
@@ -366,18 +367,39 @@ def test_batched_overflow_fallback(eng, monkeypatch):
     old, olr = O.knn(xh, q, "l2", k)
     check_topk(ld, lr, old, olr, xh, q, "l2")
     base_d, base_r = gpu_search(eng, x, q, "cosine", k)
-    monkeypatch.setenv("FX_BATCH_FORCE_FALLBACK", "1")
-    fd, fr = gpu_search(eng, x, q, "cosine", k)
+    with _lib.options(force_fallback=1):
+        fd, fr = gpu_search(eng, x, q, "cosine", k)
     od, orow = O.knn(xh, q, "cosine", k)
     check_topk(fd, fr, od, orow, xh, q, "cosine")
     check_topk(base_d, base_r, od, orow, xh, q, "cosine")
-    monkeypatch.setenv("FX_BATCH_FORCE_FALLBACK", "0")
-    monkeypatch.setenv("FX_BATCH_CAP", str(16 * k))  # tiny buffers: more phases
-    sd, sr = gpu_search(eng, x, q, "cosine", k)
+    np.testing.assert_array_equal(fr, base_r)
+    np.testing.assert_array_equal(fd.view(np.uint32), base_d.view(np.uint32))
+    with _lib.options(batch_cap=16 * k):  # tiny buffers: more phases
+        sd, sr = gpu_search(eng, x, q, "cosine", k)
     check_topk(sd, sr, od, orow, xh, q, "cosine")
 
 
-def test_batched_equals_unbatched(eng, monkeypatch):
+@pytest.mark.parametrize("k", [10, 1000])
+def test_batched_overflow_fallback_rounds(eng, k):
+    """The device-gated fallback runs in rounds of queries (its candidate
+    lists are bounded); with every query forced through it, or only those
+    whose candidates overflow a small buffer, a batch larger than a round
+    equals the per-query scans bit for bit, and no call waits for the host."""
+    n, d, nq = 60_000, 128, 300
+    x = gpu_fill(eng, n, d, seed=13)
+    q = O.fill_normal(nq, d, seed=14)
+    with _lib.options(batched=0):
+        sd, sr = gpu_search(eng, x, q, "l2", k)
+    syncs = _lib.host_sync_count()
+    for opts in ({"force_fallback": 1}, {"batch_cap": 16 * k}):
+        with _lib.options(**opts):
+            fd, fr = gpu_search(eng, x, q, "l2", k)
+        np.testing.assert_array_equal(fr, sr)
+        np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
+    assert _lib.host_sync_count() == syncs
+
+
+def test_batched_equals_unbatched(eng):
     """The MFMA path and the per-query scan agree (ids; distances to f32
     rounding — and bit for bit for L2, whose candidates are rescored with the
     scan's own summation order)."""
@@ -386,10 +408,9 @@ def test_batched_equals_unbatched(eng, monkeypatch):
     q = O.fill_normal(nq, d, seed=12)
     xh = O.fill_normal(n, d, 11)
     for metric in ("cosine", "l2"):
-        monkeypatch.delenv("FX_BATCH", raising=False)
         bd, br = gpu_search(eng, x, q, metric, k)
-        monkeypatch.setenv("FX_BATCH", "0")
-        sd, sr = gpu_search(eng, x, q, metric, k)
+        with _lib.options(batched=0):
+            sd, sr = gpu_search(eng, x, q, metric, k)
         od, orow = O.knn(xh, q, metric, k)
         check_topk(bd, br, od, orow, xh, q, metric)
         check_topk(sd, sr, od, orow, xh, q, metric)
@@ -401,69 +422,57 @@ def test_batched_equals_unbatched(eng, monkeypatch):
 
 
 @pytest.mark.parametrize("metric", METRICS)
-@pytest.mark.parametrize("n,d,nq,k,ring", [
-    (100_000, 768, 40, 100, "1"),
-    (30_011, 100, 300, 7, "1"),     # d not a multiple of the 32-deep K chunk
-    (30_011, 100, 300, 7, "0"),     # the register-staged filter kernel
-    (257, 64, 9, 300, "1"),         # n < k, a single partial tile
-    (40_000, 128, 2, 50, "0"),      # the smallest batch (64-query tiles)
-    (40_000, 128, 64, 50, "1"),     # the largest 64-query tile
-    (40_000, 128, 65, 50, "0"),     # the smallest 128-query tile
-    (40_000, 128, 128, 50, "0"),    # the largest 128-query tile
-    (40_000, 128, 129, 50, "0"),    # the smallest 256-query tile
-    (40_000, 128, 100, 50, "1"),    # the ring keeps 256-query tiles
+@pytest.mark.parametrize("n,d,nq,k", [
+    (100_000, 768, 40, 100),
+    (30_011, 100, 300, 7),     # d not a multiple of the 32-deep K chunk
+    (257, 64, 9, 300),         # n < k, a single partial tile
+    (40_000, 128, 2, 50),      # the smallest batch (64-query tiles)
+    (40_000, 128, 64, 50),     # the largest 64-query tile
+    (40_000, 128, 65, 50),     # the smallest 128-query tile
+    (40_000, 128, 128, 50),    # the largest 128-query tile
+    (40_000, 128, 129, 50),    # the smallest 256-query tile
 ])
-def test_batched_filter_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq, k, ring):
+def test_batched_filter_bit_identical_to_scan(eng, metric, n, d, nq, k):
     """fp16-MFMA filter + exact rescoring == the single-query f32 scan, bit for
-    bit (rows and distances), and the fp32-MFMA batch kernel agrees on ids."""
+    bit (rows and distances), and both pass the oracle rule.  (The filter
+    image is off here: test_filter_image_bit_identical covers it.)"""
     x = gpu_fill(eng, n, d, seed=21)
     q = O.fill_normal(nq, d, seed=22)
-    monkeypatch.delenv("FX_BATCH", raising=False)
-    monkeypatch.delenv("FX_BATCH_FILTER", raising=False)
-    monkeypatch.setenv("FX_FILTER_RING", ring)
-    fd, fr = gpu_search(eng, x, q, metric, k)
-    monkeypatch.setenv("FX_BATCH", "0")
-    sd, sr = gpu_search(eng, x, q, metric, k)
+    os.environ["FENIX_AMD_FILTER_IMAGE"] = "0"
+    try:
+        fd, fr = gpu_search(eng, x, q, metric, k)
+    finally:
+        del os.environ["FENIX_AMD_FILTER_IMAGE"]
+    with _lib.options(batched=0):
+        sd, sr = gpu_search(eng, x, q, metric, k)
     np.testing.assert_array_equal(fr, sr)
     np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
-    monkeypatch.delenv("FX_BATCH")
-    monkeypatch.setenv("FX_BATCH_FILTER", "0")
-    md, mr = gpu_search(eng, x, q, metric, k)
     xh = O.fill_normal(n, d, 21)
     od, orow = O.knn(xh, q, metric, k)
-    check_topk(md, mr, od, orow, xh, q, metric)
     check_topk(fd, fr, od, orow, xh, q, metric)
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
-def test_batched_filter_sampling_plan_invariant(eng, monkeypatch, dtype):
+def test_batched_filter_sampling_plan_invariant(eng, dtype):
     """The nested sample phases only set thresholds: any candidate buffer size
-    and sample ratio (FX_BATCH_CAP / FX_BATCH_R, e.g. 2-5 phases) gives the
-    same rows and distances, bit for bit (every kept candidate is rescored)."""
+    and sample ratio ("batch_cap" / "batch_sample_ratio", e.g. 2-5 phases)
+    gives the same rows and distances, bit for bit (every kept candidate is
+    rescored)."""
     n, d, nq, k = 400_000, 256, 96, 50
     tdt = torch.float16 if dtype == "f16" else torch.float32
     x = gpu_fill(eng, n, d, seed=31, dtype=tdt)
     q = O.fill_normal(nq, d, seed=32)
     if dtype == "f16":
         q = q.astype(np.float16).astype(np.float32)
-    for v in ("FX_BATCH", "FX_BATCH_FILTER", "FX_BATCH_CAP", "FX_BATCH_R", "FX_FILTER_RING"):
-        monkeypatch.delenv(v, raising=False)
     for metric in METRICS:
         base_d, base_r = gpu_search(eng, x, q, metric, k)
-        for cap, r in (("", "3"), ("", "8"), ("32768", ""), (str(16 * k), "2")):
-            for var, val in (("FX_BATCH_CAP", cap), ("FX_BATCH_R", r)):
-                if val:
-                    monkeypatch.setenv(var, val)
-                else:
-                    monkeypatch.delenv(var, raising=False)
-            pd, pr = gpu_search(eng, x, q, metric, k)
+        for cap, r in ((0, 3), (0, 8), (32768, 0), (16 * k, 2)):
+            with _lib.options(batch_cap=cap, batch_sample_ratio=r):
+                pd, pr = gpu_search(eng, x, q, metric, k)
             np.testing.assert_array_equal(pr, base_r)
             np.testing.assert_array_equal(pd.view(np.uint32), base_d.view(np.uint32))
-        monkeypatch.delenv("FX_BATCH_CAP", raising=False)
-        monkeypatch.delenv("FX_BATCH_R", raising=False)
-        monkeypatch.setenv("FX_BATCH", "0")
-        sd, sr = gpu_search(eng, x, q, metric, k)
-        monkeypatch.delenv("FX_BATCH")
+        with _lib.options(batched=0):
+            sd, sr = gpu_search(eng, x, q, metric, k)
         np.testing.assert_array_equal(base_r, sr)
         np.testing.assert_array_equal(base_d.view(np.uint32), sd.view(np.uint32))
 
@@ -471,26 +480,20 @@ def test_batched_filter_sampling_plan_invariant(eng, monkeypatch, dtype):
 @pytest.mark.parametrize("metric", METRICS)
 @pytest.mark.parametrize("n,d,nq,k", [(120_000, 1536, 24, 1000), (20_003, 104, 64, 10),
                                       (30_000, 200, 100, 40), (50_000, 768, 256, 100)])
-@pytest.mark.parametrize("ring", ["0", "1"])
-def test_batched_f16_corpus_bit_identical_to_scan(eng, monkeypatch, metric, n, d, nq, k, ring):
-    """fp16 columns (configs[4]'s dtype) in a batch: the filter (register-
-    staged kernel, or the LDS-DMA ring) reads the rows exactly; results equal
-    the per-query f16 scan bit for bit."""
+def test_batched_f16_corpus_bit_identical_to_scan(eng, metric, n, d, nq, k):
+    """fp16 columns (configs[4]'s dtype) in a batch: the filter reads the rows
+    exactly; results equal the per-query f16 scan bit for bit."""
     x = gpu_fill(eng, n, d, seed=23, dtype=torch.float16)
     q = O.fill_normal(nq, d, seed=24).astype(np.float16).astype(np.float32)
-    monkeypatch.delenv("FX_BATCH", raising=False)
-    monkeypatch.delenv("FX_BATCH_FILTER", raising=False)
-    monkeypatch.setenv("FX_FILTER_RING", ring)
     fd, fr = gpu_search(eng, x, q, metric, k)
-    monkeypatch.setenv("FX_BATCH", "0")
-    sd, sr = gpu_search(eng, x, q, metric, k)
+    with _lib.options(batched=0):
+        sd, sr = gpu_search(eng, x, q, metric, k)
     np.testing.assert_array_equal(fr, sr)
     np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
 
 
 @pytest.mark.parametrize("metric", METRICS)
-@pytest.mark.parametrize("ring", ["1", "0"])
-def test_batched_filter_extreme_rows_and_queries(eng, monkeypatch, metric, ring):
+def test_batched_filter_extreme_rows_and_queries(eng, metric):
     """Rows the fp16 filter cannot bound (|x| >= 65504, inf, NaN) are forced
     through; tiny-magnitude rows and queries scaled by 2^+-60 still bound
     correctly: results equal the scan's bit for bit."""
@@ -511,21 +514,22 @@ def test_batched_filter_extreme_rows_and_queries(eng, monkeypatch, metric, ring)
     q[2] = xh[big[0]]                      # a query out of fp16 range
     q[3] = xh[big[12]]                     # a tiny query
     q[4] = 0.0
-    monkeypatch.delenv("FX_BATCH", raising=False)
-    monkeypatch.setenv("FX_FILTER_RING", ring)
-    fd, fr = gpu_search(eng, x, q, metric, k)
-    monkeypatch.setenv("FX_BATCH", "0")
-    sd, sr = gpu_search(eng, x, q, metric, k)
-    np.testing.assert_array_equal(fr, sr)
-    np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
+    for image in ("1", "0"):
+        os.environ["FENIX_AMD_FILTER_IMAGE"] = image
+        try:
+            fd, fr = gpu_search(eng, x, q, metric, k)
+        finally:
+            del os.environ["FENIX_AMD_FILTER_IMAGE"]
+        with _lib.options(batched=0):
+            sd, sr = gpu_search(eng, x, q, metric, k)
+        np.testing.assert_array_equal(fr, sr)
+        np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
 
 
 @pytest.mark.parametrize("metric", METRICS)
-@pytest.mark.parametrize("ring", ["0", "1"])
-def test_batched_f16_extreme_rows_and_queries(eng, monkeypatch, metric, ring):
+def test_batched_f16_extreme_rows_and_queries(eng, metric):
     """fp16 columns with +-inf, NaN, zero, subnormal and near-max rows, and
-    queries scaled by 2^+-40: the batched path (either filter kernel) equals
-    the scan."""
+    queries scaled by 2^+-40: the batched path equals the scan."""
     n, d, k = 20_000, 64, 25
     xh = O.fill_normal(n, d, 33).astype(np.float16)
     rs = np.random.RandomState(6)
@@ -543,11 +547,9 @@ def test_batched_f16_extreme_rows_and_queries(eng, monkeypatch, metric, ring):
     q[2] = xh[sel[35]].astype(np.float32)  # a near-max query
     q[3] = xh[sel[2]].astype(np.float32)   # a subnormal query
     q[4] = 0.0
-    monkeypatch.delenv("FX_BATCH", raising=False)
-    monkeypatch.setenv("FX_FILTER_RING", ring)
     fd, fr = gpu_search(eng, x, q, metric, k)
-    monkeypatch.setenv("FX_BATCH", "0")
-    sd, sr = gpu_search(eng, x, q, metric, k)
+    with _lib.options(batched=0):
+        sd, sr = gpu_search(eng, x, q, metric, k)
     np.testing.assert_array_equal(fr, sr)
     np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
 
@@ -585,12 +587,9 @@ def _build_image(x, n, d):
 
 
 def _image_rows(img, n, d):
-    """[n, d] fp16 rows of a filter image: the MFMA-fragment layout
-    [tile][k-step][lane half][row in tile][8] (the default, padding zero) or
-    row-major (FX_IMAGE_TILED=0)."""
+    """[n, d] fp16 rows of a filter image in the MFMA-fragment layout
+    [tile][k-step][lane half][row in tile][8] (padding zero)."""
     h = img.cpu().numpy()
-    if os.environ.get("FX_IMAGE_TILED", "1") == "0":
-        return h.reshape(n, d)
     t, ks = (n + 31) // 32, (d + 15) // 16
     full = h.reshape(t, ks, 2, 32, 8).transpose(0, 3, 1, 2, 4).reshape(t * 32, ks * 16)
     assert not full[n:].any() and not full[:, d:].any(), "image padding is not zero"
@@ -635,47 +634,39 @@ def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k):
     q = O.fill_normal(nq, d, seed=44)
     q[0] *= 2.0 ** 50
     q[min(1, nq - 1)] = xh[7] if nq > 1 else q[0]
-    for v in ("FX_BATCH", "FX_BATCH_FILTER", "FX_FILTER_RING", "FENIX_AMD_FILTER_IMAGE",
-              "FX_IMAGE_TILED"):
-        monkeypatch.delenv(v, raising=False)
+    monkeypatch.delenv("FENIX_AMD_FILTER_IMAGE", raising=False)
     assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, nq, k, _lib.METRICS[metric])
-    eng._images.clear()
-    id_, ir = gpu_search(eng, x, q, metric, k)  # MFMA-fragment-order image (default)
+    eng.clear_images()
+    id_, ir = gpu_search(eng, x, q, metric, k)  # MFMA-fragment-order image
     assert id(x) in eng._images  # the image path ran
-    monkeypatch.setenv("FX_IMAGE_TILED", "0")  # row-major image, register-staged kernels
-    eng._images.clear()
-    rd, rr_ = gpu_search(eng, x, q, metric, k)
-    eng._images.clear()
-    monkeypatch.delenv("FX_IMAGE_TILED")
+    eng.clear_images()
     monkeypatch.setenv("FENIX_AMD_FILTER_IMAGE", "0")
     nd, nr = gpu_search(eng, x, q, metric, k)
-    monkeypatch.setenv("FX_BATCH", "0")
-    sd, sr = gpu_search(eng, x, q, metric, k)
-    for dd, rr in ((id_, ir), (rd, rr_), (nd, nr)):
+    with _lib.options(batched=0):
+        sd, sr = gpu_search(eng, x, q, metric, k)
+    for dd, rr in ((id_, ir), (nd, nr)):
         np.testing.assert_array_equal(rr, sr)
         np.testing.assert_array_equal(dd.view(np.uint32), sd.view(np.uint32))
 
 
 @pytest.mark.parametrize("metric", METRICS)
 def test_single_query_through_filter_image(eng, monkeypatch, metric):
-    """FX_BATCH_MIN=1: single queries take the batched filter over the image
-    (64-query tiles, one live query) and still equal the scan bit for bit."""
+    """"batch_min_queries" = 1: single queries take the batched filter over
+    the image (64-query tiles, one live query) and still equal the scan bit
+    for bit."""
     n, d, k = 80_000, 256, 100
     xh = _extreme_rows(n, d, 45)
     x = torch.from_numpy(xh).to(eng.device)
-    for v in ("FX_BATCH", "FX_BATCH_FILTER", "FX_FILTER_RING", "FENIX_AMD_FILTER_IMAGE"):
-        monkeypatch.delenv(v, raising=False)
-    monkeypatch.setenv("FX_BATCH_MIN", "1")
-    assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, 1, k, _lib.METRICS[metric])
-    for seed in (46, 47):
-        q = O.fill_normal(1, d, seed=seed)
-        fd, fr = gpu_search(eng, x, q, metric, k)
-        monkeypatch.setenv("FX_BATCH", "0")
-        sd, sr = gpu_search(eng, x, q, metric, k)
-        monkeypatch.delenv("FX_BATCH")
-        np.testing.assert_array_equal(fr, sr)
-        np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
-    monkeypatch.delenv("FX_BATCH_MIN")
+    monkeypatch.delenv("FENIX_AMD_FILTER_IMAGE", raising=False)
+    with _lib.options(batch_min_queries=1):
+        assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, 1, k, _lib.METRICS[metric])
+        for seed in (46, 47):
+            q = O.fill_normal(1, d, seed=seed)
+            fd, fr = gpu_search(eng, x, q, metric, k)
+            with _lib.options(batched=0):
+                sd, sr = gpu_search(eng, x, q, metric, k)
+            np.testing.assert_array_equal(fr, sr)
+            np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
     assert not _lib.filter_image_used(n, d, _lib.DTYPE_F32, 1, k, _lib.METRICS[metric])
 
 
@@ -684,20 +675,18 @@ def test_filter_image_follows_corpus_changes(eng, monkeypatch):
     torch update and a rewrite through Engine.fill both rebuild it, so the
     batched results keep equalling the scan's."""
     n, d, nq, k = 50_000, 128, 32, 20
-    for v in ("FX_BATCH", "FX_BATCH_FILTER", "FX_FILTER_RING", "FENIX_AMD_FILTER_IMAGE"):
-        monkeypatch.delenv(v, raising=False)
+    monkeypatch.delenv("FENIX_AMD_FILTER_IMAGE", raising=False)
     x = gpu_fill(eng, n, d, seed=51)
     q = O.fill_normal(nq, d, seed=52)
     gpu_search(eng, x, q, "l2", k)
     first = eng._images[id(x)][1]
     for change in (lambda: x.mul_(-0.5), lambda: eng.fill(x, 53)):
         change()
-        monkeypatch.delenv("FX_BATCH", raising=False)
         bd, br = gpu_search(eng, x, q, "l2", k)
         assert eng._images[id(x)][1] is not first
         first = eng._images[id(x)][1]
-        monkeypatch.setenv("FX_BATCH", "0")
-        sd, sr = gpu_search(eng, x, q, "l2", k)
+        with _lib.options(batched=0):
+            sd, sr = gpu_search(eng, x, q, "l2", k)
         np.testing.assert_array_equal(br, sr)
         np.testing.assert_array_equal(bd.view(np.uint32), sd.view(np.uint32))
     key = id(x)
@@ -840,30 +829,27 @@ def test_large_k_exceeding_rows_and_multi_shard_merge(eng):
                                        (200_003, 1536, torch.float16), (80_001, 256, torch.float32),
                                        (70_000, 1000, torch.float32)])
 @pytest.mark.parametrize("metric", METRICS)
-def test_interleaved_scan_equals_contiguous(eng, monkeypatch, n, d, dtype, metric):
-    """Block steps dealt round-robin over the grid (FX_SCAN_INTERLEAVE=1, the
+def test_interleaved_scan_equals_contiguous(eng, n, d, dtype, metric):
+    """Block steps dealt round-robin over the grid ("scan_interleave" 1, the
     default for rows of >= 1 KB) and one contiguous range per block give the
     same top-k bit for bit: unmasked, masked, row-list scans, several single
-    queries per launch (FX_BATCH=0), and distance mode."""
+    queries per launch ("batched" 0), and distance mode."""
     x = gpu_fill(eng, n, d, seed=71, dtype=dtype, cluster=500)
     q = torch.from_numpy(O.fill_normal(3, d, seed=72)).to(eng.device)
     keep = np.random.RandomState(7).rand(n) < 0.3
     m = device_mask(keep, eng.device)
     mid = _lib.METRICS[metric]
     k = min(64, n)
-    monkeypatch.setenv("FX_BATCH", "0")
     out = {}
-    for il in ("0", "1"):
-        monkeypatch.setenv("FX_SCAN_INTERLEAVE", il)
-        for pipe in ("1", "0"):
-            monkeypatch.setenv("FX_SCAN_PIPE", pipe)
+    for il in (0, 1):
+        with _lib.options(batched=0, scan_interleave=il):
             res = [eng.search([Shard(x, 11)], q, mid, k),
                    eng.search([Shard(x, 11)], q, mid, k, [m]),
                    eng.search([Shard(x, 11)], q, mid, k, [m], [int(keep.sum())]),
                    (eng.distances(Shard(x, 11), q, mid),)]
             torch.cuda.synchronize()
-            out[(il, pipe)] = [tuple(t.cpu().numpy() for t in r) for r in res]
-    ref = out[("0", "1")]
+        out[il] = [tuple(t.cpu().numpy() for t in r) for r in res]
+    ref = out[0]
     for key, got in out.items():
         for a, b in zip(ref, got):
             for ta, tb in zip(a, b):

@@ -88,9 +88,10 @@ def test_quint8_over_flight(qenv, tmp_path):
 
 
 @pytest.mark.parametrize("metric", METRICS)
-def test_quint8_dma_ring_equals_register_tiles(qenv, monkeypatch, metric):
+def test_quint8_dma_ring_equals_register_tiles(qenv, metric):
     """The LDS-DMA ring (unmasked scans) and the register tiles (masked scans,
-    FX_Q8_DMA=0) compute the same distances bit for bit, top-k and all rows."""
+    option "q8_dma" 0) compute the same distances bit for bit, top-k and all
+    rows."""
     from fenix_amd import _lib
     from fenix_amd.engine import Engine, Shard
 
@@ -99,12 +100,11 @@ def test_quint8_dma_ring_equals_register_tiles(qenv, monkeypatch, metric):
     shard = Shard(codes, 0, float(qenv["type"].scale), int(qenv["type"].shift))
     q = torch.from_numpy(O.fill_normal(1, qenv["d"], seed=74))
     m = _lib.METRICS[metric]
-    monkeypatch.delenv("FX_Q8_DMA", raising=False)
     dd, dr = eng.search([shard], q, m, 50)
     da = eng.distances(shard, q, m)
-    monkeypatch.setenv("FX_Q8_DMA", "0")
-    rd, rr = eng.search([shard], q, m, 50)
-    ra = eng.distances(shard, q, m)
+    with _lib.options(q8_dma=0):
+        rd, rr = eng.search([shard], q, m, 50)
+        ra = eng.distances(shard, q, m)
     assert torch.equal(dr, rr)
     assert torch.equal(dd.view(torch.int32), rd.view(torch.int32))
     assert torch.equal(da.view(torch.int32), ra.view(torch.int32))
