@@ -11,8 +11,14 @@ Mirrors src/fenix/flight.py of the reference:
   ``drop_table``, ``search`` (:242-288: metric assert, pickled descriptor,
   ``pa.table({"target": ...})`` over ``do_exchange``) and ``remove``.
 
-The wire format (descriptor dict, ``target`` column, result schema) is
-unchanged, so a reference client can talk to this server and vice versa.
+The wire format (descriptor dict, ``target`` column, result schema, action
+names and their pickled bodies) is unchanged, so a reference client can talk
+to this server and vice versa.  Only ``search`` / ``do_exchange`` / ``do_put``
+are on the accelerated path; the admin surface is kept for drop-in use and
+written here as tables: server actions dispatch through ``Server._ACTIONS``,
+the read options that ``read_table`` sets before a ``do_get`` live in one
+locked dict (``Server._read_opts``, not attributes of the server object), and
+the client issues every action through ``Flight._action``.
 ``io.index.call`` underneath runs on the GPU (fenix_amd.io.index), as do the
 coded-index actions (``make-coder``, ``make-index``, ``drop-index``,
 :82-101: k-means training, table encoding and probe search, io.coder /
@@ -42,10 +48,16 @@ from . import io
 
 
 class Server(fl.FlightServerBase):
+    # read_table's per-read options, set and cleared by "set-*" / "del-*"
+    # actions around a do_get (flight.py:105-131 of the reference); the value
+    # of each lives under the action body's key of the same name
+    _READ_OPTS = ("coding", "column", "filter", "select")
+
     def __init__(self, root: str, host: str = "0.0.0.0", port: int = 9001) -> None:
         self.root = os.path.abspath(root)
         self.grpc = f"grpc://{host}:{port}"
-        self._attr_lock = threading.Lock()
+        self._opts_lock = threading.Lock()
+        self._read_opts: dict = {}
 
         super().__init__(location=self.grpc)
 
@@ -66,26 +78,20 @@ class Server(fl.FlightServerBase):
         reader: fl.MetadataRecordBatchReader,
         writer: fl.FlightMetadataWriter,
     ) -> None:
-        name = descriptor.path[0].decode()
-        data = reader.to_reader()
-
-        # rewriting the file changes its (size, mtime): the HBM copy is restaged
-        io.table.make(self.root, name, data)
+        # an atomic rewrite bumps the file version: the HBM copy is restaged
+        io.table.make(self.root, descriptor.path[0].decode(), reader.to_reader())
 
     def do_get(self, ctx: fl.ServerCallContext, ticket: fl.Ticket):
-        source = ticket.ticket.decode().split(":")
-
-        if hasattr(self, "coding") and hasattr(self, "column"):
-            data = io.index.load(self.root, self.coding, source, self.column)
+        sources = ticket.ticket.decode().split(":")
+        with self._opts_lock:
+            opts = dict(self._read_opts)
+        if "coding" in opts and "column" in opts:
+            data = io.index.load(self.root, opts["coding"], sources, opts["column"])
         else:
-            data = io.table.load(self.root, source)
-
-        if hasattr(self, "filter"):
-            data = data.filter(self.filter)
-
-        if hasattr(self, "select"):
-            data = data.select(self.select)
-
+            data = io.table.load(self.root, sources)
+        for key, apply in (("filter", pa.Table.filter), ("select", pa.Table.select)):
+            if key in opts:
+                data = apply(data, opts[key])
         return fl.GeneratorStream(data.schema, data.to_reader())
 
     def do_exchange(
@@ -96,7 +102,6 @@ class Server(fl.FlightServerBase):
         writer: fl.MetadataRecordBatchWriter,
     ) -> None:
         config = pickle.loads(descriptor.command)
-
         config["target"] = reader.read_all().column("target").combine_chunks()
         config["filter"] = pickle.loads(config["filter"])
 
@@ -105,60 +110,39 @@ class Server(fl.FlightServerBase):
         writer.begin(data.schema)
         writer.write_table(data)
 
+    # ------------------------------------------------------------- actions
+    def _drop_index(self, name: str) -> None:
+        io.coder.drop(self.root, name)
+        for path in io.index.list(self.root):
+            if path.endswith("/" + name):
+                os.unlink(os.path.join(self.root, io.index.LOCATION, path + ".arrow"))
+
+    _ACTIONS = {
+        "make-coder": lambda self, b: io.coder.make(self.root, **b),
+        "make-index": lambda self, b: io.index.make(self.root, **b),
+        "drop-index": lambda self, b: self._drop_index(**b),
+        "drop-table": lambda self, b: io.table.drop(self.root, **b),
+        "remove": lambda self, b: shutil.rmtree(self.root),
+    }
+
     def do_action(self, ctx: fl.ServerCallContext, action: fl.Action) -> None:
-        config = pickle.loads(action.body.to_pybytes())
+        verb, _, key = action.type.partition("-")
+        handler = self._ACTIONS.get(action.type)
+        if handler is None and not (verb in ("set", "del") and key in self._READ_OPTS):
+            raise ValueError()
+        body = pickle.loads(action.body.to_pybytes())
+        if handler is not None:
+            handler(self, body)
+            return
+        with self._opts_lock:
+            if verb == "set":
+                self._read_opts[key] = body[key]
+            else:
+                self._read_opts.pop(key, None)
 
-        match action.type:
-            case "make-coder":
-                io.coder.make(self.root, **config)
 
-            case "make-index":
-                io.index.make(self.root, **config)
-
-            case "drop-index":
-                io.coder.drop(self.root, **config)
-
-                suffix = "/" + config["name"]
-                for path in io.index.list(self.root):
-                    if path.endswith(suffix):
-                        os.unlink(os.path.join(self.root, io.index.LOCATION, path + ".arrow"))
-
-            case "drop-table":
-                io.table.drop(self.root, **config)
-
-            case "remove":
-                shutil.rmtree(self.root)
-
-            case "set-coding":
-                self.coding = config["coding"]
-
-            case "del-coding":
-                if hasattr(self, "coding"):
-                    delattr(self, "coding")
-
-            case "set-column":
-                self.column = config["column"]
-
-            case "del-column":
-                if hasattr(self, "column"):
-                    delattr(self, "column")
-
-            case "set-filter":
-                self.filter = config["filter"]
-
-            case "del-filter":
-                if hasattr(self, "filter"):
-                    delattr(self, "filter")
-
-            case "set-select":
-                self.select = config["select"]
-
-            case "del-select":
-                if hasattr(self, "select"):
-                    delattr(self, "select")
-
-            case _:
-                raise ValueError()
+# the metric names Flight.search accepts (coder.py:38-50 and their aliases)
+METRICS = frozenset({"cosine", "dot", "inner_product", "l2", "euclidean"})
 
 
 @dataclass(frozen=True)
@@ -174,15 +158,17 @@ class Flight:
         if "conn" in self.__dict__:
             self.conn.close()
 
+    def _action(self, action: str, **body) -> Self:
+        """One admin action: its name and a pickled dict body (the reference's
+        wire format)."""
+        self.conn.do_action(fl.Action(action, pickle.dumps(body)))
+        return self
+
     def make_table(self, name: str, data: pa.RecordBatchReader) -> Self:
-        descriptor = fl.FlightDescriptor.for_path(name)
-
-        writer, reader = self.conn.do_put(descriptor, data.schema)
-
+        writer, _ = self.conn.do_put(fl.FlightDescriptor.for_path(name), data.schema)
         with writer:
             for batch in data:
                 writer.write_batch(batch)
-
         return self
 
     def read_table(
@@ -193,60 +179,32 @@ class Flight:
         select: Sequence[str] | None = None,
         filter: pc.Expression | None = None,
     ) -> pa.RecordBatchReader:
+        opts = {"select": select, "filter": filter}
         if coding is not None and column is not None:
-            self.conn.do_action(fl.Action("set-coding", pickle.dumps({"coding": coding})))
-            self.conn.do_action(fl.Action("set-column", pickle.dumps({"column": column})))
-
-        if select is not None:
-            self.conn.do_action(fl.Action("set-select", pickle.dumps({"select": select})))
-
-        if filter is not None:
-            self.conn.do_action(fl.Action("set-filter", pickle.dumps({"filter": filter})))
-
-        source = ":".join(source) if not isinstance(source, str) else source
-        ticket = fl.Ticket(source)
-        reader = self.conn.do_get(ticket).to_reader()
-
-        self.conn.do_action(fl.Action("del-coding", pickle.dumps({})))
-        self.conn.do_action(fl.Action("del-column", pickle.dumps({})))
-        self.conn.do_action(fl.Action("del-select", pickle.dumps({})))
-        self.conn.do_action(fl.Action("del-filter", pickle.dumps({})))
-
+            opts.update(coding=coding, column=column)
+        for key, value in opts.items():
+            if value is not None:
+                self._action(f"set-{key}", **{key: value})
+        names = source if isinstance(source, str) else ":".join(source)
+        reader = self.conn.do_get(fl.Ticket(names)).to_reader()
+        for key in ("coding", "column", "select", "filter"):
+            self._action(f"del-{key}")
         return reader
 
     def drop_table(self, name: str) -> Self:
-        self.conn.do_action(fl.Action("drop-table", pickle.dumps({"name": name})))
-
-        return self
+        return self._action("drop-table", name=name)
 
     def make_index(
         self, name: str, source: str | Sequence[str], column: str, config: dict
     ) -> Self:
-        self.conn.do_action(
-            fl.Action(
-                "make-coder",
-                pickle.dumps({"name": name, "source": source, "column": column, "config": config}),
-            )
-        )
-
+        self._action("make-coder", name=name, source=source, column=column, config=config)
         return self.sync_index(name, source, column)
 
     def sync_index(self, name: str, source: str | Sequence[str], column: str) -> Self:
-        self.conn.do_action(
-            fl.Action(
-                "make-index",
-                pickle.dumps({"name": name, "source": source, "column": column}),
-            )
-        )
-
-        return self
+        return self._action("make-index", name=name, source=source, column=column)
 
     def drop_index(self, name: str) -> Self:
-        self.conn.do_action(
-            fl.Action("drop-index", pickle.dumps({"name": name})),
-        )
-
-        return self
+        return self._action("drop-index", name=name)
 
     def search(
         self,
@@ -260,42 +218,26 @@ class Flight:
         maxval: int | None = None,
         probes: int | None = None,
     ) -> pa.Table:
-        METRICS: set[str] = {"cosine", "dot", "inner_product", "l2", "euclidean"}
-
+        """The drop-in search (flight.py:242-288 of the reference): the same
+        assert, descriptor dict (filter pickled twice) and ``target`` table."""
         assert metric in METRICS
 
-        descriptor = fl.FlightDescriptor.for_command(
-            pickle.dumps(
-                {
-                    "coding": coding,
-                    "source": source,
-                    "column": column,
-                    "metric": metric,
-                    "select": select,
-                    "filter": pickle.dumps(filter),
-                    "maxval": maxval,
-                    "probes": probes,
-                }
-            )
-        )
-
+        command = {"coding": coding, "source": source, "column": column, "metric": metric,
+                   "select": select, "filter": pickle.dumps(filter), "maxval": maxval,
+                   "probes": probes}
         if type(target).__module__.split(".")[0] == "torch":  # Tensor, without importing torch
             target = target.numpy()
-
         if isinstance(target, np.ndarray):
             target = pa.array(target)
+        table = pa.table({"target": target})
 
-        target = pa.table({"target": target})
-
-        writer, reader = self.conn.do_exchange(descriptor)
-
+        writer, reader = self.conn.do_exchange(
+            fl.FlightDescriptor.for_command(pickle.dumps(command)))
         with writer:
-            writer.begin(target.schema)
-            writer.write_table(target)
+            writer.begin(table.schema)
+            writer.write_table(table)
             writer.done_writing()
-
             return reader.read_all()
 
     def remove(self) -> Self:
-        self.conn.do_action(fl.Action("remove", pickle.dumps({})))
-        return self
+        return self._action("remove")

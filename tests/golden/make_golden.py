@@ -2,7 +2,7 @@
 
 Run ONLY in the build container, where the reference checkout exists:
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [--only-g6]
 
 It imports fenix from /root/reference/src (Python 3.10 needs the
 ``typing.Self`` shim: fenix/flight.py:5 imports it, fenix wants >= 3.11),
@@ -55,7 +55,7 @@ def _import_fenix():
 
 def _batches(x: np.ndarray, chunk: int):
     d = x.shape[1]
-    vt = pa.list_(pa.float32(), list_size=d)
+    vt = pa.list_(pa.from_numpy_dtype(x.dtype), list_size=d)
     schema = pa.schema({"id": pa.int64(), "vector": vt})
     out = []
     for s in range(0, x.shape[0], chunk):
@@ -97,10 +97,48 @@ def direct_case(fenix, root, name, x, chunk, queries, ks, metrics=METRICS, meta=
     return rec
 
 
+def g6_fp16(fenix, root) -> dict:
+    """G6: a 1536-d float16 column (configs[4]'s dtype and width).  The
+    reference's fp16 path works up to select_k (which crashes on a halffloat
+    key in pyarrow 25): with maxval=None it returns the UDF's own
+    per-chunk distances (index.py:133-159 -> coder.py:38-50 in ATen half
+    arithmetic) for every row, as halffloat (index.py:150-158, 165).  The
+    target is passed as float16: index.py:111's pa.scalar(target, type=...)
+    does not cast a float32 array to a halffloat list."""
+    n, d = 3000 + 111, 1536
+    x = fill_normal(n, d, seed=13, dtype=np.float16)
+    q = fill_normal(4, d, seed=14).astype(np.float16)
+    schema, batches = _batches(x, 1000)
+    fenix.io.table.make(root, "g6_fp16", pa.RecordBatchReader.from_batches(schema, batches))
+    rec = {}
+    metrics = ["l2", "cosine", "inner_product"]
+    for metric in metrics:
+        out = np.empty((len(q), n), dtype=np.float16)
+        for i, qv in enumerate(q):
+            t = fenix.io.index.call(root, None, "g6_fp16", "vector", target=qv, metric=metric)
+            assert t.schema.field("__DISTANCE__").type == pa.float16()
+            np.testing.assert_array_equal(t.column("id").to_numpy(), np.arange(n))
+            out[i] = t.column("__DISTANCE__").to_numpy()
+            rec["schema"] = str(t.schema)
+        rec[f"{metric}_all_dist"] = out
+    meta = dict(kind="direct_full_table_fp16", n=n, d=d, seed=13, qseed=14, nq=4, chunk=1000,
+                cluster=0, dtype="float16", sha256=_sha(x), metrics=metrics)
+    np.savez_compressed(os.path.join(HERE, "g6_fp16.npz"), meta=json.dumps(meta), **rec)
+    return meta
+
+
 def main() -> None:
     fenix = _import_fenix()
     root = tempfile.mkdtemp(prefix="fenix_golden_")
     manifest = {}
+    if "--only-g6" in sys.argv:  # add the fp16 case to an existing manifest
+        with open(os.path.join(HERE, "MANIFEST.json")) as f:
+            manifest = json.load(f)
+        manifest["g6_fp16"] = g6_fp16(fenix, root)
+        with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        print("wrote g6_fp16")
+        return
 
     # G1: generic N(0,1)-like corpora, ragged last chunk (8192 = 8*1000 + 192)
     for d in (128, 768):
@@ -166,6 +204,8 @@ def main() -> None:
                 sha256=_sha(x), ks=[10], metrics=METRICS)
     np.savez_compressed(os.path.join(HERE, "g4_flight.npz"), meta=json.dumps(meta), **rec)
     manifest["g4_flight"] = meta
+
+    manifest["g6_fp16"] = g6_fp16(fenix, root)
 
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

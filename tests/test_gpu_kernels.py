@@ -82,6 +82,48 @@ def test_golden_fenix_ids_and_distances(eng, golden_dir, name):
             assert rel.max() <= 1e-5, f"{name} {metric} k={k}: rel {rel.max():.3e}"
 
 
+def test_golden_fp16_full_table(eng, golden_dir):
+    """G6 (tests/golden/g6_fp16.npz): the reference's own __DISTANCE__ column
+    for a 1536-d halffloat corpus with maxval=None (index.py:150-165, ATen
+    half arithmetic) against the engine's (fp16 loads, fp32 accumulation,
+    rounded to halffloat) through io.index.call: within one fp16 ulp (and
+    2^-14 |q||x| for inner products, tests/test_oracle_golden.fp16_tolerance),
+    and within one ulp of the float64 oracle rounded to fp16.  The size of
+    the half-accumulation difference is recorded in gpurun_out."""
+    import pyarrow as pa
+    from fenix_amd.io import index
+    from tests.test_oracle_golden import fp16_tolerance
+
+    z, meta = _golden(golden_dir, "g6_fp16")
+    n, d = meta["n"], meta["d"]
+    x = O.fill_normal(n, d, meta["seed"], dtype=np.float16)
+    q = O.fill_normal(meta["nq"], d, meta["qseed"]).astype(np.float16)
+    vt = pa.list_(pa.float16(), list_size=d)
+    batches = [pa.record_batch([pa.array(np.arange(s, min(s + 1000, n))),
+                                pa.FixedSizeListArray.from_arrays(
+                                    pa.array(x[s:s + 1000].ravel()), list_size=d)],
+                               names=["id", "vector"]) for s in range(0, n, 1000)]
+    src = pa.Table.from_batches(batches, pa.schema({"id": pa.int64(), "vector": vt}))
+    stats = {}
+    for metric in meta["metrics"]:
+        ref = z[f"{metric}_all_dist"]
+        got = np.stack([index.call("", None, src, "vector", target=qv, metric=metric)
+                        .column("__DISTANCE__").to_numpy() for qv in q])
+        assert got.dtype == np.float16
+        err = np.abs(got.astype(np.float64) - ref.astype(np.float64))
+        tol = fp16_tolerance(ref, metric, q.astype(np.float32), x)
+        assert np.all(err <= tol), (metric, float((err / tol).max()))
+        o16 = O.distances(x, q.astype(np.float32), metric).astype(np.float32).astype(np.float16)
+        ulp = np.spacing(np.abs(o16)).astype(np.float64)
+        assert np.all(np.abs(got.astype(np.float64) - o16.astype(np.float64)) <= ulp), metric
+        stats[metric] = {"max_err_vs_reference_in_tolerance": float((err / tol).max()),
+                         "frac_equal_to_reference": float((err == 0).mean()),
+                         "max_abs_err_vs_reference": float(err.max())}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "g6_fp16_stats.json"), "w") as f:
+        json.dump(stats, f, indent=1)
+
+
 def test_golden_ties(eng, golden_dir):
     """Duplicated rows: fenix pins the tie SET; we also pin the order (row asc)."""
     z, meta = _golden(golden_dir, "g2_ties")

@@ -21,7 +21,23 @@ import pytest
 
 from oracle import oracle as O
 
-NAMES = ["g1_d128", "g1_d768", "g2_ties", "g3_tail", "g4_flight"]
+NAMES = ["g1_d128", "g1_d768", "g2_ties", "g3_tail", "g4_flight", "g6_fp16"]
+
+
+def fp16_tolerance(ref16, metric, q, x):
+    """Agreement of two fp16 __DISTANCE__ columns computed with different
+    accumulations (the reference: ATen half arithmetic, coder.py:38-50; the
+    oracle: float64; the engine: fp32): one fp16 ulp of the value, and for
+    inner products, whose small results cancel large terms, 2^-14 of the
+    summed magnitude |q||x|.  Measured on g6_fp16 (reference vs float64
+    rounded to fp16): l2 <= 1 ulp, cosine <= 1 ulp, inner product
+    <= 2.1e-5 |q||x| (5 ulps of a near-zero value)."""
+    ulp = np.spacing(np.abs(ref16).astype(np.float16)).astype(np.float64)
+    if metric in ("inner_product", "dot"):
+        sc = np.linalg.norm(np.asarray(q, np.float64), axis=1)[:, None] * \
+            np.linalg.norm(np.asarray(x, np.float64), axis=1)[None, :]
+        return np.maximum(ulp, 2.0 ** -14 * sc)
+    return ulp
 
 
 def load(golden_dir, name):
@@ -30,6 +46,8 @@ def load(golden_dir, name):
 
 
 def corpus(meta):
+    if meta.get("dtype") == "float16":
+        return O.fill_normal(meta["n"], meta["d"], meta["seed"], dtype=np.float16)
     if meta.get("duplicate"):
         base = O.fill_normal(meta["n"] // 2, meta["d"], meta["seed"])
         return np.concatenate([base, base])
@@ -134,3 +152,19 @@ def test_fenix_distance_restatement_matches_reference(golden_dir):
                 chunk = x[c0 : c0 + 1000]
                 dv = O.fenix_distance(q[i], chunk, metric)[0, r - c0]
                 assert np.float32(dv) == fd[i, j]
+
+
+def test_fp16_full_table_matches_reference(golden_dir):
+    """G6: the reference's own fp16 distances (maxval=None over a 1536-d
+    halffloat column, ATen half arithmetic) against the float64 oracle
+    rounded to fp16, at fp16 resolution (fp16_tolerance)."""
+    z, meta = load(golden_dir, "g6_fp16")
+    x = corpus(meta)
+    q = O.fill_normal(meta["nq"], meta["d"], meta["qseed"]).astype(np.float16).astype(np.float32)
+    assert "__DISTANCE__: halffloat" in str(z["schema"])
+    for metric in meta["metrics"]:
+        ref = z[f"{metric}_all_dist"]
+        o16 = O.distances(x, q, metric).astype(np.float32).astype(np.float16)
+        err = np.abs(o16.astype(np.float64) - ref.astype(np.float64))
+        assert np.all(err <= fp16_tolerance(ref, metric, q, x)), metric
+        assert (err == 0).mean() > 0.8, metric  # mostly the same half
