@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                   help="library option (fx_set_option), e.g. batch_sample_ratio=20; sweeps only")
     return p.parse_args()
 
 
@@ -201,6 +203,9 @@ def main():
     from fenix_amd.engine import Engine, Shard
 
     eng = Engine.get(device)
+    for o in args.opt:
+        name, value = o.split("=", 1)
+        _lib.set_option(name, int(value))
     qu8 = args.dtype == "qu8"
     tdt = {"f32": torch.float32, "f16": torch.float16, "qu8": torch.uint8}[args.dtype]
     esize = {"f32": 4, "f16": 2, "qu8": 1}[args.dtype]
@@ -356,6 +361,7 @@ def main():
                 "k": k,
                 "queries": nq,
                 "metric": args.metric,
+                **({"options": args.opt} if args.opt else {}),
                 "parallelism": f"row-shard x{world}"
                 + ((" + gloo all-gather" if gloo else " + RCCL all-gather") if use_dist else ""),
             },

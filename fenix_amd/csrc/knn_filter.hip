@@ -87,6 +87,14 @@ namespace FX_FILTER_IMPL {
 #ifndef FX_FILTER_BK
 #define FX_FILTER_BK (FX_FILTER_BQ >= 256 ? 32 : 64)  // >= 1 query piece per thread
 #endif
+#ifndef FX_FILTER_IMG3  // the 256-query, 32-wide-K build (knn_filter.hip itself):
+                        // filter_img3_kernel serves tiled filter images
+#if FX_FILTER_BQ == 256 && FX_FILTER_BK == 32
+#define FX_FILTER_IMG3 1
+#else
+#define FX_FILTER_IMG3 0
+#endif
+#endif
 constexpr int fBM = FX_FILTER_BM;               // corpus rows per tile
 constexpr int fBQ = FX_FILTER_BQ;               // queries per block
 constexpr int fBK = FX_FILTER_BK;               // K chunk (elements)
@@ -1080,7 +1088,7 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img2_kernel(Filte
 #endif
 }
 
-#if FX_FILTER_IMG2
+#if FX_FILTER_IMG2 && !FX_FILTER_IMG3
 static int launch_img2(const FilterArgs& a, int metric, hipStream_t stream) {
   const size_t smem = sizeof(Img2Shared);
   const void* fn = metric == FX_METRIC_COS ? (const void*)filter_img2_kernel<2>
@@ -1114,6 +1122,882 @@ static int launch_img2(const FilterArgs& a, int metric, hipStream_t stream) {
   return check_launch("filter_img2_kernel");
 }
 #endif  // FX_FILTER_IMG2
+
+// ------------------------------------- tiled image, query tile by LDS-DMA ring
+#if FX_FILTER_IMG3
+//
+// filter_img3_kernel: filter_img2_kernel's tiling (8 waves, wave w owns the
+// 32-row tile w of a 256-row tile against all 256 queries, A fragments
+// straight from the tiled image into registers) with the query tile moved by
+// LDS-DMA (buffer_load ... lds) instead of through registers and ds_write:
+//   * the K chunks of the query tile are the same for every row tile, so the
+//     chunk sequence runs on across tiles in one ring of FX_I3_QA + 1 slots,
+//     FX_I3_QA chunks in flight, one raw s_barrier per chunk behind a counted
+//     vmcnt (cdna_hip_programming.md: pipelining across barriers);
+//   * 16-B pieces XOR-swizzled by query ((q >> 2) & 3) on the global side:
+//     the B-fragment ds_read_b128 are conflict-free without row padding;
+//   * the image stream runs on across tiles too: FX_I3_XS register stages,
+//     the next tile's first chunks issued as the current tile's last ones
+//     are multiplied, so they stream in during its epilogue;
+//   * the rows' image sums (and mask words) are loaded at the tile's first
+//     chunk, every thread the same count (counted waits stay exact);
+//   * appends go to per-query LDS segments (no returning global atomic,
+//     which would wait for the prefetched stream: vmcnt retires in order),
+//     flushed at the end;
+//   * the pass test is packed: per pair of rows one v_pk_fma_f32 gives
+//     RN(x - a rv) and one v_pk_add_f32 subtracts b; the sign collects the
+//     fail bit (2 instructions per (row, query) instead of 3).
+#ifndef FX_I3_QA
+#define FX_I3_QA 3   // query chunks in flight (ring of FX_I3_QA + 1 slots)
+#endif
+#ifndef FX_I3_XS
+#define FX_I3_XS 2   // image chunks in flight per wave (register stages)
+#endif
+#ifndef FX_I3_SEG
+#define FX_I3_SEG 24  // LDS append entries per query (overflow: global slots)
+#endif
+#ifndef FX_I3_XPF
+#define FX_I3_XPF 1   // the next tile's first image chunks in flight during the epilogue
+#endif
+constexpr int kI3Slots = FX_I3_QA + 1;
+constexpr int kI3QBytes = fBQ * fBK * 2;               // one slot: 16 KB
+constexpr int kI3QDma = kI3QBytes / 1024 / fWaves;     // 1-KB DMAs per wave per chunk
+static_assert(kI3QDma * 1024 * fWaves == kI3QBytes && fBK == 32, "query ring");
+struct Img3Shared {
+  unsigned char qring[kI3Slots][kI3QBytes];
+  float rinfo[fBM];
+  float rterm[fBM];
+  uint32_t rflags[2][kRowFlagWords];
+  f32x4 qtab[fBQ];
+  float2 qab[fBQ];
+  uint32_t seg[fBQ + 3 * fBQ * FX_I3_SEG];  // counters, then entries {lb key, ub key, row}
+  uint32_t segbase[fBQ];
+};
+static_assert(sizeof(Img3Shared) <= 160 * 1024, "filter_img3_kernel: LDS over 160 KB");
+
+typedef __attribute__((address_space(3))) void* i3_lds_ptr;
+
+template <int N>
+__device__ __forceinline__ void i3_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// The pass test and appends of one wave's 32-row tile (RT = 1) against all
+// kI2QT query tiles; appends into LDS segments (filter_epilogue_seg's layout).
+template <int METRIC>
+__device__ __forceinline__ void i3_epilogue(const f32x16 (&acc)[kI2QT], const float* rinfo,
+                                            const float* rterm, const uint32_t* flags,
+                                            const f32x4* qtab, const float2* qab,
+                                            const FilterArgs& a, int64_t q0, int64_t r0, int wid,
+                                            int h, int l32, uint32_t* seg, int diag) {
+  constexpr int SEG = FX_I3_SEG;
+  // row j of the lane (accumulator element j) is local row lr0 + (j & 3) + 8 (j >> 2)
+  const int lr0 = wid * 32 + 4 * h;
+  f32x4 rv4[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) rv4[g] = *reinterpret_cast<const f32x4*>(rinfo + lr0 + 8 * g);
+  const uint32_t fmask = flags[wid * 2 + h], smask = flags[16 + wid * 2 + h];
+  uint32_t pm[kI2QT];
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u) {
+    const float2 ab = qab[u * 32 + l32];
+    const f32x2 na = {-ab.x, -ab.x}, nb = {-ab.y, -ab.y};
+    // fail bit j = sign of RN(RN(x_j - a rv_j) - b): set exactly when x_j -
+    // a rv_j rounds below b (NaN passes); bit j enters last-in at bit 0
+    uint32_t fail = 0u;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      const f32x4 r = rv4[i >> 1];
+      const f32x2 rp = (i & 1) ? f32x2{r[2], r[3]} : f32x2{r[0], r[1]};
+      const f32x2 xp = {acc[u][2 * i], acc[u][2 * i + 1]};
+      const f32x2 dd = __builtin_elementwise_fma(na, rp, xp) + nb;
+      fail = __builtin_amdgcn_alignbit(fail, __float_as_uint(dd[1]), 31);
+      fail = __builtin_amdgcn_alignbit(fail, __float_as_uint(dd[0]), 31);
+    }
+    pm[u] = (diag & 1) ? 0u : (~fail | fmask) & ~smask & 0xffffu;
+    if (q0 + u * 32 + l32 >= a.nq) pm[u] = 0u;
+  }
+  uint32_t any = 0u;
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u) any |= pm[u];
+  if (__ballot(any != 0u) == 0ull) return;
+  // Appends (a few per wave and tile): per query tile with a pass, a loop
+  // over the lane's set bits; the row's accumulator element is selected by
+  // a cndmask tree (a dynamic index would put the accumulators in scratch,
+  // and a scratch load waits for the whole prefetched stream), its row
+  // value re-read from LDS.  static_for over u for the same reason.
+  static_for<kI2QT>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    if (__ballot(pm[u] != 0u) == 0ull) return;
+    const int qi = u * 32 + l32;
+    const int64_t gq = q0 + qi;
+    uint32_t bits = pm[u];
+    uint32_t p = bits != 0u ? atomicAdd(&seg[qi], (uint32_t)__popc(bits)) : 0u;
+    const f32x4 qc = qtab[qi];
+    const float qc1 = qc[0], qc0 = qc[1], qA = qc[2], qB = qc[3];
+    const bool fq = !(qA <= 3.4e38f);
+    uint32_t gp = ~0u;
+    while (bits != 0u) {
+      const int j = __builtin_ctz(bits);
+      const uint32_t rest = bits;
+      bits &= bits - 1u;
+      // (bit-field selects, v_bfi_b32: a ?: select tree is turned back into
+      // a dynamic index, i.e. scratch)
+      auto pick = [](float lo, float hi, uint32_t m) {
+        return __uint_as_float((__float_as_uint(hi) & m) | (__float_as_uint(lo) & ~m));
+      };
+      const uint32_t m0 = 0u - ((uint32_t)j & 1u), m1 = 0u - (((uint32_t)j >> 1) & 1u);
+      const uint32_t m2 = 0u - (((uint32_t)j >> 2) & 1u), m3 = 0u - (((uint32_t)j >> 3) & 1u);
+      float v8[8], v4[4], v2[2];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v8[i] = pick(acc[u][2 * i], acc[u][2 * i + 1], m0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v4[i] = pick(v8[2 * i], v8[2 * i + 1], m1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) v2[i] = pick(v4[2 * i], v4[2 * i + 1], m2);
+      const float x = pick(v2[0], v2[1], m3);
+      const int lr = lr0 + (j & 3) + 8 * (j >> 2);
+      const float rv = rinfo[lr];
+      float lb, ub;
+      if constexpr (METRIC == 0) {
+        const float s2 = rv + qc0;
+        const float d2 = fmaf(x, qc1, s2);
+        const float e = fmaf(qA, s2, qB);
+        lb = sqrtf(fmaxf(d2 - e, 0.f));
+        ub = sqrtf(d2 + e);
+      } else if constexpr (METRIC == 1) {
+        const float e = fmaf(qA, rv, qB);
+        lb = fmaf(x, qc1, -e);
+        ub = fmaf(x, qc1, e);
+      } else {
+        const float rt = rterm[lr];
+        const float dist = fmaf(x * rt, qc1, 0.5f);
+        const float e = fmaf(qB, rt, qA);
+        lb = dist - e;
+        ub = dist + e;
+      }
+      if (fq || rv != rv) {  // forced: below / above every key
+        lb = -__builtin_inff();
+        ub = __builtin_nanf("");
+      }
+      const uint32_t grow = (uint32_t)(a.row_base + r0) + (uint32_t)lr;
+      if (p < (uint32_t)SEG) {
+        uint32_t* e = seg + fBQ + 3 * (qi * SEG + p);
+        e[0] = order_key(lb);
+        e[1] = order_key(ub);
+        e[2] = grow;
+      } else {  // rare: past the segment, global slots for the lane's remaining passes
+        if (gp == ~0u) gp = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(rest));
+        if (gp < (uint32_t)a.cap) {
+          const size_t slot = (size_t)gq * a.cap + gp;
+          if (a.cand_ub != nullptr) {
+            a.cand[slot] = make_comp(lb, grow);
+            a.cand_ub[slot] = make_comp(ub, grow);
+          } else {
+            a.cand[slot] = make_comp(ub, grow);
+          }
+        }
+        ++gp;
+      }
+      ++p;
+    }
+  });
+}
+
+template <int METRIC>
+__global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(FilterArgs a) {
+  constexpr int XS = FX_I3_XS, SEG = FX_I3_SEG;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Img3Shared* sh = reinterpret_cast<Img3Shared*>(smem);
+#ifdef FX_DIAG_BUILD  // FX_FILTER_DIAG: 1 no appends, 2 no epilogue, 4 no MFMA,
+                      // 8 no query DMA, 16 no step barrier, 32 no image loads
+  const int diag = a.diag;
+#else
+  constexpr int diag = 0;
+#endif
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, l32 = lane & 31;
+  const int64_t q0 = (int64_t)blockIdx.y * fBQ;
+  // chunks per tile, padded to a multiple of the register stages (past the
+  // row end the image reads zeros and the query tile is zero-padded to dq)
+  const int nch = ((a.d + fBK - 1) / fBK + XS - 1) / XS * XS;
+  const int ksteps = (a.d + 15) / 16;
+  const int64_t ntile32 = (a.n + 31) / 32;
+  if ((int64_t)blockIdx.x >= a.num_tiles) return;
+  filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
+  for (int q = tid; q < fBQ; q += fThreads) sh->seg[q] = 0u;  // (ordered by the first barrier)
+
+  // the query tile, blocked by 32 components (FilterArgs::Qh); chunk c of
+  // query q is 64 B at (c * qstride + q) * 64
+  const __amdgpu_buffer_rsrc_t qr = [&] {
+    const uint64_t qp = reinterpret_cast<uint64_t>(a.Qh + q0 * 32);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)qp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(qp >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane(
+        (int)(((int64_t)(a.dq / 32 - 1) * a.qstride + fBQ) * 64));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             nb, 0x00020000);
+  }();
+  // this lane's piece of each of the wave's DMAs: query 16 j + lane / 4, slot
+  // piece lane % 4 holding global piece (lane % 4) ^ ((q >> 2) & 3)
+  uint32_t qv[kI3QDma];
+#pragma unroll
+  for (int i = 0; i < kI3QDma; ++i) {
+    const int j = wid * kI3QDma + i;
+    const int q = 16 * j + (lane >> 2);
+    qv[i] = (uint32_t)(q * 64 + (((lane & 3) ^ ((q >> 2) & 3)) * 16));
+  }
+  auto issue_q = [&](int c, int slot) {
+    if (diag & 8) return;
+    unsigned char* st = sh->qring[slot];
+#pragma unroll
+    for (int i = 0; i < kI3QDma; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (i3_lds_ptr)(st + (wid * kI3QDma + i) * 1024), 16,
+                                               qv[i], (int)(c * a.qstride * 64), 0, 0);
+  };
+  // this wave's 32-row tile of the row tile at step iteration ti: its
+  // k-steps, one KB each (a tile past the end: an empty descriptor, zeros)
+  auto x_rsrc = [&](int64_t ti) {
+    const int64_t t32 = (a.tile_start + ti * a.tile_stride) * (fBM / 32) + wid;
+    const int64_t live = (ti < a.num_tiles && t32 < ntile32) ? 1 : 0;
+    const unsigned char* base = reinterpret_cast<const unsigned char*>(a.X) +
+                                (live ? t32 : 0) * (int64_t)ksteps * 1024;
+    const uint64_t xp = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xp >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)(live * ksteps * 1024));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             nb, 0x00020000);
+  };
+  const uint32_t xl = (uint32_t)opaque(lane) * 16u;
+  typedef f16x8 XA[kI2KS];
+  auto load_x = [&](XA& xa, __amdgpu_buffer_rsrc_t xr, int c) {
+    if (diag & 32) {
+#pragma unroll
+      for (int s = 0; s < kI2KS; ++s) xa[s] = f16x8((_Float16)0.f);
+      return;
+    }
+#pragma unroll
+    for (int s = 0; s < kI2KS; ++s) {
+      const int ks = c * kI2KS + s;  // wave-uniform: past the row end reads zeros
+      const uint32_t off = ks < ksteps ? xl : 0x7fff0000u;
+      xa[s] = __builtin_bit_cast(
+          f16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, ks * 1024, 2 /* nt */));
+    }
+  };
+  // B fragment of query tile u, k-step s of a slot: query Q = 32 u + l32,
+  // global piece 2 s + h at its swizzled place
+  uint32_t bq[kI2KS];
+#pragma unroll
+  for (int s = 0; s < kI2KS; ++s) {
+    const int Q = (int)opaque((unsigned)l32);
+    bq[s] = (uint32_t)(Q * 64 + (((2 * s + h) ^ ((Q >> 2) & 3)) * 16));
+  }
+  f32x16 acc[kI2QT];
+  auto compute = [&](const XA& xa, int slot) {
+    if (diag & 4) {  // (diagnostics: no MFMA; the row loads stay live)
+      if (xa[0][0] == (_Float16)1.2345f && xa[kI2KS - 1][7] == (_Float16)2.f) a.count[0] = 7;
+      return;
+    }
+    const unsigned char* st = sh->qring[slot];
+#pragma unroll
+    for (int s = 0; s < kI2KS; ++s) {
+#pragma unroll
+      for (int u = 0; u < kI2QT; ++u) {
+        // (query tile u sits 32 x 64 B further: (Q + 32 u) has the same swizzle)
+        const f16x8 bv = *reinterpret_cast<const f16x8*>(st + bq[s] + u * 32 * 64);
+        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bv, acc[u], 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- prologue: query chunks 0 .. QA-1 and image chunks 0 .. XS-1 of the
+  // first tile in flight
+  int qc = 0, qslot = 0;  // next query chunk to issue and its slot
+#pragma unroll
+  for (int i = 0; i < FX_I3_QA; ++i) {
+    issue_q(qc, qslot);
+    qc = qc + 1 == nch ? 0 : qc + 1;
+    qslot = qslot + 1 == kI3Slots ? 0 : qslot + 1;
+  }
+  XA xa[XS];
+  int64_t xt = blockIdx.x;  // tile (iteration index) of the next image chunk to load
+  int xc = 0;
+  __amdgpu_buffer_rsrc_t xr = x_rsrc(xt);
+  static_for<XS>([&](auto sc) {
+    load_x(xa[decltype(sc)::value], xr, xc);
+    if (++xc == nch) {
+      xc = 0;
+      xt += gridDim.x;
+      xr = x_rsrc(xt);
+    }
+  });
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (once: the prologue's order differs)
+  int rslot = 0;  // slot of the query chunk the next step reads
+  int par = 0;
+  const int lr = tid & (fBM - 1);  // the row this thread notes (threads >= fBM: duplicates)
+  for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
+    const int64_t r0 = (a.tile_start + ti * a.tile_stride) * fBM;
+    if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;  // (read two tiles back)
+#pragma unroll
+    for (int u = 0; u < kI2QT; ++u) acc[u] = f32x16(0.f);
+    float rsum = 0.f;
+    uint32_t mword = 0u;
+    // one K step: multiply chunk c + S, then (LOAD) refill its register
+    // stage with the chunk XS steps ahead (the next tile's first chunks at
+    // the end of a tile, FX_I3_XPF)
+    auto step = [&](int c, auto sc, auto ld) {
+      constexpr int S = decltype(sc)::value;
+      // query chunk c + S landed (this wave's DMAs; the loads issued after
+      // it: the image chunk of its step, then QA - 1 steps of both), and
+      // every wave done with the slot refilled next
+      if (diag & 16)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else
+        i3_wait_barrier<kI2KS + (FX_I3_QA - 1) * (kI3QDma + kI2KS)>();
+      issue_q(qc, qslot);
+      qc = qc + 1 == nch ? 0 : qc + 1;
+      qslot = qslot + 1 == kI3Slots ? 0 : qslot + 1;
+      if (S == 0 && c == 0) {  // the rows' image sums and mask words of this tile
+        const int64_t row = r0 + lr < a.n ? r0 + lr : a.n - 1;
+        rsum = a.rowinfo[row];
+        // (both kernel arguments: global loads; a pointer to a __device__
+        // constant made a flat load, which counts in lgkmcnt too, and the
+        // step's LDS waits then waited for it)
+        const bool masked = a.mask != nullptr;
+        const uint32_t* mp = masked ? a.mask + (row >> 5)
+                                    : reinterpret_cast<const uint32_t*>(a.rowinfo) + row;
+        mword = *mp | (masked ? 0u : ~0u);
+      }
+      compute(xa[S], rslot);
+      rslot = rslot + 1 == kI3Slots ? 0 : rslot + 1;
+      if constexpr (decltype(ld)::value) {
+        load_x(xa[S], xr, xc);
+        if (++xc == nch) {
+          xc = 0;
+          xt += gridDim.x;
+          xr = x_rsrc(xt);
+        }
+      }
+    };
+    using Load = std::true_type;
+    int c = 0;
+    for (; c + XS < nch; c += XS)
+      static_for<XS>([&](auto sc) { step(c, sc, Load{}); });
+    static_for<XS>([&](auto sc) { step(c, sc, std::integral_constant<bool, FX_I3_XPF>{}); });
+    if (tid < fBM) {  // one thread per row: bound factor, flags
+      // (the row index recomputed here from opaque(tid): hoisted out of the
+      // tile loop, its flag bit was spilled and reloaded behind a vmcnt(0))
+      const int lr = (int)opaque((unsigned)tid);
+      const int64_t row = r0 + lr;
+      bool ok = row < a.n && ((mword >> (row & 31)) & 1u);
+      const float s = ok ? rsum : 0.f;
+      float rv;
+      if constexpr (METRIC == 0) {
+        rv = s;
+      } else if constexpr (METRIC == 1) {
+        rv = sqrtf(s);
+      } else {
+        rv = fmaxf(sqrtf(s), 1e-12f);
+      }
+      if (!(s <= 3.4e38f)) rv = __builtin_nanf("");
+      filter_note_row<METRIC, 1>(sh->rinfo, sh->rterm, sh->rflags[par], lr, rv, ok);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (diag & 2) {
+      if (acc[0][0] == 1.2345f) a.count[0] = 7;
+    } else {
+      i3_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rflags[par], sh->qtab, sh->qab, a, q0,
+                          r0, wid, h, l32, sh->seg, diag);
+    }
+    if constexpr (!FX_I3_XPF) {  // the next tile's first chunks, after the epilogue
+      static_for<XS>([&](auto sc) {
+        load_x(xa[decltype(sc)::value], xr, xc);
+        if (++xc == nch) {
+          xc = 0;
+          xt += gridDim.x;
+          xr = x_rsrc(xt);
+        }
+      });
+    }
+  }
+  // the ring's and the stream's last loads (past the end) land before the
+  // workgroup's LDS is released; then the segments go out
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  filter_flush_segments<SEG>(sh->seg, sh->segbase, a, q0, tid);
+}
+
+static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
+  const size_t smem = sizeof(Img3Shared);
+  const void* fn = metric == FX_METRIC_COS ? (const void*)filter_img3_kernel<2>
+                   : metric == FX_METRIC_IP ? (const void*)filter_img3_kernel<1>
+                                            : (const void*)filter_img3_kernel<0>;
+  if (int rc = allow_lds(fn)) return rc;
+  int cus = 0;
+  int rc = device_cus(&cus);
+  if (rc) return rc;
+  const int64_t qtiles = (a.nq + fBQ - 1) / fBQ;
+  int64_t bx = cus;
+  if (bx > a.num_tiles) bx = a.num_tiles;
+  for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
+    FilterArgs b = a;
+    const int64_t yn = (qtiles - y0) < 65535 ? (qtiles - y0) : 65535;
+    b.Qh = a.Qh + y0 * fBQ * 32;
+    b.qinfo = a.qinfo + y0 * fBQ * 4;
+    b.thr = a.thr + y0 * fBQ;
+    b.count = a.count + y0 * fBQ * kCountStride;
+    b.cand = a.cand + y0 * fBQ * (int64_t)a.cap;
+    if (a.cand_ub) b.cand_ub = a.cand_ub + y0 * fBQ * (int64_t)a.cap;
+    b.nq = a.nq - y0 * fBQ;
+    void* args[] = {(void*)&b};
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(fThreads), args,
+                                   smem, stream);
+    if (e != hipSuccess) {
+      set_error("filter_img3_kernel launch: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+  }
+  return check_launch("filter_img3_kernel");
+}
+#endif  // FX_FILTER_IMG3
+
+// ------------------------- tiled image, one wave per SIMD, 64-row wave tiles
+#if !FX_FILTER_IMG3  // (the 256-query, 32-wide-K build only)
+#undef FX_FILTER_IMG4
+#define FX_FILTER_IMG4 0
+#endif
+#ifndef FX_FILTER_IMG4
+#define FX_FILTER_IMG4 0
+#endif
+#if FX_FILTER_IMG4
+//
+// filter_img4_kernel: filter_img3_kernel with 4 waves of 512 registers (one
+// per SIMD) instead of 8 of 256.  Wave w owns rows 64 w .. + 63 of the
+// 256-row tile (two 32-row MFMA row tiles) against all 256 queries: 256
+// accumulator registers, and every B fragment read from the query ring feeds
+// two MFMAs (half the LDS reads per MFMA).  The register room holds
+// FX_I4_XS image chunks in flight.  Appends store the raw product, the row
+// value and the row in the LDS segment; their bounds are computed when the
+// segments are flushed.
+#ifndef FX_I4_XS
+#define FX_I4_XS 3
+#endif
+#ifndef FX_I4_SEG
+#define FX_I4_SEG 20  // LDS append entries per query (overflow: global slots)
+#endif
+constexpr int kI4Waves = 4, kI4Threads = 64 * kI4Waves;
+struct Img4Shared {
+  unsigned char qring[kI3Slots][kI3QBytes];
+  float rinfo[fBM];
+  uint32_t rflags[2][kRowFlagWords];
+  f32x4 qtab[fBQ];
+  float2 qab[fBQ];
+  float stage[kI4Waves][16 * 64];  // per wave: one query tile's accumulators, [element][lane]
+  uint32_t seg[fBQ + 3 * fBQ * FX_I4_SEG];  // counters, then raw entries {x, rv, row}
+  uint32_t segbase[fBQ];
+  float rterm[fBM];  // (cosine: written by filter_note_row, the bounds use 1 / rv)
+};
+static_assert(sizeof(Img4Shared) <= 160 * 1024, "filter_img4_kernel: LDS over 160 KB");
+constexpr int kI4QDma = kI3QBytes / 1024 / kI4Waves;  // 1-KB query DMAs per wave per chunk
+constexpr int kI4XLd = 2 * kI2KS;                     // image loads per wave per chunk
+static_assert(kI4QDma * 1024 * kI4Waves == kI3QBytes && kI4Waves * 64 == fBM, "img4 tiling");
+
+// [lb, ub] of a (row, query) pair from the fp16 product x, the row value rv
+// (cosine max(|x|, 1e-12), IP |x|, L2 |x|^2; NaN: forced) and the query's
+// {c1, c0, A, B} (filter_query_table)
+template <int METRIC>
+__device__ __forceinline__ void i4_bounds(float x, float rv, const f32x4& qc, float& lb,
+                                          float& ub) {
+  const float qc1 = qc[0], qc0 = qc[1], qA = qc[2], qB = qc[3];
+  if constexpr (METRIC == 0) {
+    const float s2 = rv + qc0;
+    const float d2 = fmaf(x, qc1, s2);
+    const float e = fmaf(qA, s2, qB);
+    lb = sqrtf(fmaxf(d2 - e, 0.f));
+    ub = sqrtf(d2 + e);
+  } else if constexpr (METRIC == 1) {
+    const float e = fmaf(qA, rv, qB);
+    lb = fmaf(x, qc1, -e);
+    ub = fmaf(x, qc1, e);
+  } else {
+    const float rt = 1.f / rv;
+    const float dist = fmaf(x * rt, qc1, 0.5f);
+    const float e = fmaf(qB, rt, qA);
+    lb = dist - e;
+    ub = dist + e;
+  }
+  if (!(qA <= 3.4e38f) || rv != rv) {  // forced: below / above every key
+    lb = -__builtin_inff();
+    ub = __builtin_nanf("");
+  }
+}
+
+// One accumulator element, read from its AGPR by v_accvgpr_read: a plain
+// VALU use makes the allocator copy whole accumulator tuples into VGPRs
+// (and spill them); the "a" operand keeps them where the MFMAs wrote them.
+// (The epilogue runs behind the tile's last barrier, far past the MFMA's
+// write latency.)
+__device__ __forceinline__ float acc_rd(float v) {
+  float r;
+  asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(v));
+  return r;
+}
+
+// Pass test and appends of the 32-row group g of the tile (lanes' rows
+// 32 g + 4 h + (j & 3) + 8 (j >> 2)) against all kI2QT query tiles.  A query
+// tile with a pass has its accumulators staged in the wave's LDS rows
+// (stage[element][lane]); each lane then walks its set bits with dynamic
+// LDS reads (a dynamic register index would be scratch).
+template <int METRIC>
+__device__ __forceinline__ void i4_epilogue(const f32x16 (&acc)[kI2QT], int g, const float* rinfo,
+                                            const uint32_t* flags, const f32x4* qtab,
+                                            const float2* qab, const FilterArgs& a, int64_t q0,
+                                            int64_t r0, int lane, float* stage, uint32_t* seg,
+                                            int diag) {
+  constexpr int SEG = FX_I4_SEG;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int lr0 = g * 32 + 4 * h;
+  f32x4 rv4[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) rv4[i] = *reinterpret_cast<const f32x4*>(rinfo + lr0 + 8 * i);
+  const uint32_t fmask = flags[g * 2 + h], smask = flags[16 + g * 2 + h];
+  uint32_t pm[kI2QT];
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u) {
+    const float2 ab = qab[u * 32 + l32];
+    const f32x2 na = {-ab.x, -ab.x}, nb = {-ab.y, -ab.y};
+    uint32_t fail = 0u;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      const f32x4 r = rv4[i >> 1];
+      const f32x2 rp = (i & 1) ? f32x2{r[2], r[3]} : f32x2{r[0], r[1]};
+      const f32x2 xp = {acc_rd(acc[u][2 * i]), acc_rd(acc[u][2 * i + 1])};
+      const f32x2 dd = __builtin_elementwise_fma(na, rp, xp) + nb;
+      fail = __builtin_amdgcn_alignbit(fail, __float_as_uint(dd[1]), 31);
+      fail = __builtin_amdgcn_alignbit(fail, __float_as_uint(dd[0]), 31);
+    }
+    pm[u] = (diag & 1) ? 0u : (~fail | fmask) & ~smask & 0xffffu;
+    if (q0 + u * 32 + l32 >= a.nq) pm[u] = 0u;
+  }
+  uint32_t any = 0u;
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u) any |= pm[u];
+  if (__ballot(any != 0u) == 0ull) return;
+  // every query tile's segment slots at once (LDS atomics in flight together)
+  uint32_t pos[kI2QT];
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u)
+    pos[u] = pm[u] != 0u ? atomicAdd(&seg[u * 32 + l32], (uint32_t)__popc(pm[u])) : 0u;
+  const uint32_t grow0 = (uint32_t)(a.row_base + r0);
+  static_for<kI2QT>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    if (__ballot(pm[u] != 0u) == 0ull) return;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) stage[j * 64 + lane] = acc_rd(acc[u][j]);
+    const int qi = u * 32 + l32;
+    uint32_t bits = pm[u], p = pos[u], gp = ~0u;
+    while (bits != 0u) {
+      const int j = __builtin_ctz(bits);
+      const uint32_t rest = bits;
+      bits &= bits - 1u;
+      const float x = stage[j * 64 + lane];
+      const int lr = lr0 + (j & 3) + 8 * (j >> 2);
+      const float rv = rinfo[lr];
+      const uint32_t grow = grow0 + (uint32_t)lr;
+      if (p < (uint32_t)SEG) {  // raw: the bounds are computed at the flush
+        uint32_t* e = seg + fBQ + 3 * (qi * SEG + p);
+        e[0] = __float_as_uint(x);
+        e[1] = __float_as_uint(rv);
+        e[2] = grow;
+      } else {  // rare: past the segment, global slots for the lane's remaining passes
+        const int64_t gq = q0 + qi;
+        if (gp == ~0u) gp = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(rest));
+        if (gp < (uint32_t)a.cap) {
+          float lb, ub;
+          i4_bounds<METRIC>(x, rv, qtab[qi], lb, ub);
+          const size_t slot = (size_t)gq * a.cap + gp;
+          if (a.cand_ub != nullptr) {
+            a.cand[slot] = make_comp(lb, grow);
+            a.cand_ub[slot] = make_comp(ub, grow);
+          } else {
+            a.cand[slot] = make_comp(ub, grow);
+          }
+        }
+        ++gp;
+      }
+      ++p;
+    }
+  });
+}
+
+// i4_epilogue's segments to the candidate buffer: one global atomic per
+// query reserves the slots; each raw entry {x, rv, row} becomes its bounds.
+template <int METRIC>
+__device__ __forceinline__ void i4_flush(uint32_t* seg, uint32_t* base, const f32x4* qtab,
+                                         const FilterArgs& a, int64_t q0, int tid) {
+  constexpr int SEG = FX_I4_SEG;
+  __syncthreads();
+  for (int q = tid; q < fBQ; q += kI4Threads) {
+    const uint32_t n = seg[q] < (uint32_t)SEG ? seg[q] : (uint32_t)SEG;
+    seg[q] = n;
+    base[q] = n != 0u && q0 + q < a.nq ? atomicAdd(&a.count[(q0 + q) * kCountStride], n) : 0u;
+  }
+  __syncthreads();
+  for (int i = tid; i < fBQ * SEG; i += kI4Threads) {
+    const int q = i / SEG, j = i % SEG;
+    if ((uint32_t)j >= seg[q]) continue;
+    const uint32_t p = base[q] + (uint32_t)j;
+    if (p >= (uint32_t)a.cap) continue;
+    const uint32_t* e = seg + fBQ + 3 * i;
+    float lb, ub;
+    i4_bounds<METRIC>(__uint_as_float(e[0]), __uint_as_float(e[1]), qtab[q], lb, ub);
+    const size_t slot = (size_t)(q0 + q) * a.cap + p;
+    if (a.cand_ub != nullptr) {
+      a.cand[slot] = make_comp(lb, e[2]);
+      a.cand_ub[slot] = make_comp(ub, e[2]);
+    } else {
+      a.cand[slot] = make_comp(ub, e[2]);
+    }
+  }
+}
+
+template <int METRIC>
+__global__ void __launch_bounds__(kI4Threads, 1) filter_img4_kernel(FilterArgs a) {
+  constexpr int XS = FX_I4_XS;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Img4Shared* sh = reinterpret_cast<Img4Shared*>(smem);
+#ifdef FX_DIAG_BUILD  // FX_FILTER_DIAG as filter_img3_kernel
+  const int diag = a.diag;
+#else
+  constexpr int diag = 0;
+#endif
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, l32 = lane & 31;
+  const int64_t q0 = (int64_t)blockIdx.y * fBQ;
+  const int nch = ((a.d + fBK - 1) / fBK + XS - 1) / XS * XS;
+  const int ksteps = (a.d + 15) / 16;
+  const int64_t ntile32 = (a.n + 31) / 32;
+  if ((int64_t)blockIdx.x >= a.num_tiles) return;
+  filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, kI4Threads);
+  for (int q = tid; q < fBQ; q += kI4Threads) sh->seg[q] = 0u;
+  // the ring starts zeroed: a slot a chunk past the query tile's padding
+  // never receives (its DMA is dropped) then holds finite values
+  for (int i = tid; i < kI3Slots * kI3QBytes / 16; i += kI4Threads)
+    reinterpret_cast<i32x4*>(sh->qring)[i] = i32x4(0);
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t qr = [&] {
+    const uint64_t qp = reinterpret_cast<uint64_t>(a.Qh + q0 * 32);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)qp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(qp >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane(
+        (int)(((int64_t)(a.dq / 32 - 1) * a.qstride + fBQ) * 64));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             nb, 0x00020000);
+  }();
+  const int qchunks = a.dq / 32;  // chunks the query tile holds
+  uint32_t qv[kI4QDma];
+#pragma unroll
+  for (int i = 0; i < kI4QDma; ++i) {
+    const int j = wid * kI4QDma + i;
+    const int q = 16 * j + (lane >> 2);
+    qv[i] = (uint32_t)(q * 64 + (((lane & 3) ^ ((q >> 2) & 3)) * 16));
+  }
+  auto issue_q = [&](int c, int slot) {
+    if (diag & 8) return;
+    unsigned char* st = sh->qring[slot];
+#pragma unroll
+    for (int i = 0; i < kI4QDma; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          qr, (i3_lds_ptr)(st + (wid * kI4QDma + i) * 1024), 16,
+          c < qchunks ? qv[i] : 0x7fff0000u, (int)(c * a.qstride * 64), 0, 0);
+  };
+  // this wave's two 32-row tiles (adjacent in the image: one descriptor)
+  auto x_rsrc = [&](int64_t ti) {
+    const int64_t t32 = (a.tile_start + ti * a.tile_stride) * (fBM / 32) + 2 * wid;
+    int64_t live = ti < a.num_tiles ? ntile32 - t32 : 0;
+    live = live < 0 ? 0 : live > 2 ? 2 : live;
+    const unsigned char* base = reinterpret_cast<const unsigned char*>(a.X) +
+                                (live ? t32 : 0) * (int64_t)ksteps * 1024;
+    const uint64_t xp = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xp >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)(live * ksteps * 1024));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             nb, 0x00020000);
+  };
+  const uint32_t xl = (uint32_t)opaque(lane) * 16u;
+  typedef f16x8 XA[2][kI2KS];
+  auto load_x = [&](XA& xa, __amdgpu_buffer_rsrc_t xr, int c) {
+    if (diag & 32) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < kI2KS; ++s) xa[t][s] = f16x8((_Float16)0.f);
+      return;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int s = 0; s < kI2KS; ++s) {
+        const int ks = c * kI2KS + s;  // wave-uniform: past the row end reads zeros
+        const uint32_t off = ks < ksteps ? xl + (uint32_t)(t * ksteps * 1024) : 0x7fff0000u;
+        xa[t][s] = __builtin_bit_cast(
+            f16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, ks * 1024, 2 /* nt */));
+      }
+    }
+  };
+  uint32_t bq[kI2KS];
+#pragma unroll
+  for (int s = 0; s < kI2KS; ++s) {
+    const int Q = (int)opaque((unsigned)l32);
+    bq[s] = (uint32_t)(Q * 64 + (((2 * s + h) ^ ((Q >> 2) & 3)) * 16));
+  }
+  f32x16 acc[2][kI2QT];
+  auto compute = [&](const XA& xa, int slot) {
+    if (diag & 4) {
+      if (xa[0][0][0] == (_Float16)1.2345f && xa[1][kI2KS - 1][7] == (_Float16)2.f) a.count[0] = 7;
+      return;
+    }
+    const unsigned char* st = sh->qring[slot];
+#pragma unroll
+    for (int s = 0; s < kI2KS; ++s) {
+      f16x8 bv[kI2QT];
+#pragma unroll
+      for (int u = 0; u < kI2QT; ++u)
+        bv[u] = *reinterpret_cast<const f16x8*>(st + bq[s] + u * 32 * 64);
+#pragma unroll
+      for (int u = 0; u < kI2QT; ++u) {
+        acc[0][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[0][s], bv[u], acc[0][u], 0, 0, 0);
+        acc[1][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[1][s], bv[u], acc[1][u], 0, 0, 0);
+      }
+    }
+  };
+
+  int qc = 0, qslot = 0;
+#pragma unroll
+  for (int i = 0; i < FX_I3_QA; ++i) {
+    issue_q(qc, qslot);
+    qc = qc + 1 == nch ? 0 : qc + 1;
+    qslot = qslot + 1 == kI3Slots ? 0 : qslot + 1;
+  }
+  XA xa[XS];
+  int64_t xt = blockIdx.x;
+  int xc = 0;
+  __amdgpu_buffer_rsrc_t xr = x_rsrc(xt);
+  static_for<XS>([&](auto sc) {
+    load_x(xa[decltype(sc)::value], xr, xc);
+    if (++xc == nch) {
+      xc = 0;
+      xt += gridDim.x;
+      xr = x_rsrc(xt);
+    }
+  });
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int rslot = 0;
+  int par = 0;
+  for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
+    const int64_t r0 = (a.tile_start + ti * a.tile_stride) * fBM;
+    if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < kI2QT; ++u) acc[t][u] = f32x16(0.f);
+    float rsum = 0.f;
+    uint32_t mword = 0u;
+    auto step = [&](int c, auto sc) {
+      constexpr int S = decltype(sc)::value;
+      if (diag & 16)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else
+        i3_wait_barrier<kI4XLd + (FX_I3_QA - 1) * (kI4QDma + kI4XLd)>();
+      issue_q(qc, qslot);
+      qc = qc + 1 == nch ? 0 : qc + 1;
+      qslot = qslot + 1 == kI3Slots ? 0 : qslot + 1;
+      if (S == 0 && c == 0) {  // the rows' image sums and mask words of this tile
+        const int64_t row = r0 + tid < a.n ? r0 + tid : a.n - 1;
+        rsum = a.rowinfo[row];
+        const bool masked = a.mask != nullptr;
+        const uint32_t* mp = masked ? a.mask + (row >> 5)
+                                    : reinterpret_cast<const uint32_t*>(a.rowinfo) + row;
+        mword = *mp | (masked ? 0u : ~0u);
+      }
+      compute(xa[S], rslot);
+      rslot = rslot + 1 == kI3Slots ? 0 : rslot + 1;
+      load_x(xa[S], xr, xc);
+      if (++xc == nch) {
+        xc = 0;
+        xt += gridDim.x;
+        xr = x_rsrc(xt);
+      }
+    };
+    for (int c = 0; c < nch; c += XS) static_for<XS>([&](auto sc) { step(c, sc); });
+    {  // one thread per row: bound factor, flags
+      const int lr = (int)opaque((unsigned)tid);
+      const int64_t row = r0 + lr;
+      bool ok = row < a.n && ((mword >> (row & 31)) & 1u);
+      const float s = ok ? rsum : 0.f;
+      float rv;
+      if constexpr (METRIC == 0) {
+        rv = s;
+      } else if constexpr (METRIC == 1) {
+        rv = sqrtf(s);
+      } else {
+        rv = fmaxf(sqrtf(s), 1e-12f);
+      }
+      if (!(s <= 3.4e38f)) rv = __builtin_nanf("");
+      filter_note_row<METRIC, 1>(sh->rinfo, sh->rterm, sh->rflags[par], lr, rv, ok);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (diag & 2) {
+      if (acc[0][0][0] == 1.2345f) a.count[0] = 7;
+    } else {
+      const int ol = (int)opaque((unsigned)lane);
+      i4_epilogue<METRIC>(acc[0], 2 * wid, sh->rinfo, sh->rflags[par], sh->qtab, sh->qab, a, q0,
+                          r0, ol, sh->stage[wid], sh->seg, diag);
+      i4_epilogue<METRIC>(acc[1], 2 * wid + 1, sh->rinfo, sh->rflags[par], sh->qtab, sh->qab, a,
+                          q0, r0, ol, sh->stage[wid], sh->seg, diag);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  i4_flush<METRIC>(sh->seg, sh->segbase, sh->qtab, a, q0, tid);
+}
+
+static int launch_img4(const FilterArgs& a, int metric, hipStream_t stream) {
+  const size_t smem = sizeof(Img4Shared);
+  const void* fn = metric == FX_METRIC_COS ? (const void*)filter_img4_kernel<2>
+                   : metric == FX_METRIC_IP ? (const void*)filter_img4_kernel<1>
+                                            : (const void*)filter_img4_kernel<0>;
+  if (int rc = allow_lds(fn)) return rc;
+  int cus = 0;
+  int rc = device_cus(&cus);
+  if (rc) return rc;
+  const int64_t qtiles = (a.nq + fBQ - 1) / fBQ;
+  int64_t bx = cus;
+  if (bx > a.num_tiles) bx = a.num_tiles;
+  for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
+    FilterArgs b = a;
+    const int64_t yn = (qtiles - y0) < 65535 ? (qtiles - y0) : 65535;
+    b.Qh = a.Qh + y0 * fBQ * 32;
+    b.qinfo = a.qinfo + y0 * fBQ * 4;
+    b.thr = a.thr + y0 * fBQ;
+    b.count = a.count + y0 * fBQ * kCountStride;
+    b.cand = a.cand + y0 * fBQ * (int64_t)a.cap;
+    if (a.cand_ub) b.cand_ub = a.cand_ub + y0 * fBQ * (int64_t)a.cap;
+    b.nq = a.nq - y0 * fBQ;
+    void* args[] = {(void*)&b};
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(kI4Threads), args,
+                                   smem, stream);
+    if (e != hipSuccess) {
+      set_error("filter_img4_kernel launch: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+  }
+  return check_launch("filter_img4_kernel");
+}
+#endif  // FX_FILTER_IMG4
 
 #ifndef FX_FILTER_SPLIT  // measured slower (6.48 vs 6.35 ms for configs[2], same box)
 #define FX_FILTER_SPLIT 0
@@ -1464,7 +2348,11 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.num_tiles <= 0) return FX_OK;
   const bool f16 = a.dtype == FX_DTYPE_F16;
   if (a.rowinfo != nullptr && image_tiled()) {  // the image in MFMA fragment order
-#if FX_FILTER_IMG2
+#if FX_FILTER_IMG4
+    return launch_img4(a, metric, stream);
+#elif FX_FILTER_IMG3
+    return launch_img3(a, metric, stream);
+#elif FX_FILTER_IMG2
     return launch_img2(a, metric, stream);
 #else
     set_error("filter: the tiled image is not compiled into this variant");

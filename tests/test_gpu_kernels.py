@@ -88,7 +88,7 @@ def test_golden_fp16_full_table(eng, golden_dir):
     half arithmetic) against the engine's (fp16 loads, fp32 accumulation,
     rounded to halffloat) through io.index.call: within one fp16 ulp (and
     2^-14 |q||x| for inner products, tests/test_oracle_golden.fp16_tolerance),
-    and within one ulp of the float64 oracle rounded to fp16.  The size of
+    and within the same tolerance of the float64 oracle rounded to fp16.  The size of
     the half-accumulation difference is recorded in gpurun_out."""
     import pyarrow as pa
     from fenix_amd.io import index
@@ -114,8 +114,8 @@ def test_golden_fp16_full_table(eng, golden_dir):
         tol = fp16_tolerance(ref, metric, q.astype(np.float32), x)
         assert np.all(err <= tol), (metric, float((err / tol).max()))
         o16 = O.distances(x, q.astype(np.float32), metric).astype(np.float32).astype(np.float16)
-        ulp = np.spacing(np.abs(o16)).astype(np.float64)
-        assert np.all(np.abs(got.astype(np.float64) - o16.astype(np.float64)) <= ulp), metric
+        tol64 = fp16_tolerance(o16, metric, q.astype(np.float32), x)
+        assert np.all(np.abs(got.astype(np.float64) - o16.astype(np.float64)) <= tol64), metric
         stats[metric] = {"max_err_vs_reference_in_tolerance": float((err / tol).max()),
                          "frac_equal_to_reference": float((err == 0).mean()),
                          "max_abs_err_vs_reference": float(err.max())}

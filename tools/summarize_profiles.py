@@ -9,7 +9,10 @@
   kernel, converted to bytes with the two gfx950 corrections of
   MI355X_MICROARCH.md §HBM (FETCH_SIZE is in KiB; it reports exactly half of
   the bytes of a wide coalesced streaming read, so x2).  bench.py reads
-  ``hbm_bytes_per_launch`` from it for roofline.traffic.
+  ``hbm_bytes_per_launch`` from it for roofline.traffic, only when its
+  ``library_sha`` equals the loaded library's (a kernel change makes a pass
+  stale).  ``--kernel`` is a substring; with ``--per-search N`` every N
+  matching launches (the phases of one batched search) are summed.
 """
 
 from __future__ import annotations
@@ -33,6 +36,12 @@ def main() -> None:
     p.add_argument("--algo-bytes", type=float, required=True)
     p.add_argument("--kernel", default="fx::scan_kernel")
     p.add_argument("--tag", default="")
+    p.add_argument("--per-search", type=int, default=1,
+                   help="matching launches per search (summed): the filter's phases")
+    p.add_argument("--library-sha", default=None,
+                   help="SHA-256 prefix of the library the pass ran (default: hash the "
+                        "in-tree fenix_amd/lib/libfenix_knn.so, which must be that build)")
+    p.add_argument("--source-cmd", default="")
     a = p.parse_args()
     out_dir = os.path.join(ROOT, "profiles")
     os.makedirs(out_dir, exist_ok=True)
@@ -45,12 +54,22 @@ def main() -> None:
             if a.kernel in r["Kernel_Name"]:
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
         fetch = vals.get("FETCH_SIZE", [])
-        mean_kib = sum(fetch) / len(fetch)
+        searches = len(fetch) // a.per_search
+        mean_kib = sum(fetch[: searches * a.per_search]) / searches
         hbm = mean_kib * 1024 * 2
+        if a.library_sha is None:
+            import sys
+
+            sys.path.insert(0, ROOT)
+            from fenix_amd import _lib
+
+            a.library_sha = _lib.library_sha()
         rec = {
             "workload": a.workload,
             "kernel": a.kernel,
+            "library_sha": a.library_sha,
             "launches": len(fetch),
+            "launches_per_search": a.per_search,
             "FETCH_SIZE_kib_per_launch": mean_kib,
             "hbm_bytes_per_launch": hbm,
             "algorithmic_bytes_per_launch": a.algo_bytes,
@@ -58,6 +77,7 @@ def main() -> None:
             "correction": "FETCH_SIZE is KiB; x2 because gfx950 reports half the bytes of a "
                           "16-B/lane coalesced stream (MI355X_MICROARCH.md, HBM section)",
             "source": os.path.relpath(a.pmc, ROOT),
+            "command": a.source_cmd,
         }
         with open(os.path.join(out_dir, f"{pre}_pmc_{a.workload}.json"), "w") as f:
             json.dump(rec, f, indent=1)
