@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--dtype", default="f32", choices=["f32", "f16", "qu8"],
                    help="qu8: quint8 codes (ex/arrow/quint8), scanned by fx_knn_search_ex")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-verify", action="store_true",
+                   help="skip the sortedness check (diagnostic builds that drop work)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -252,7 +254,7 @@ def main():
             return eng.merge(gd, gr, k)
         return od, orow
 
-    # a batched f32 search streams the corpus's fp16 filter image, built once
+    # a batched f32 search streams the corpus's filter image, built once
     # per corpus version: timed here, apart from the steps (reported in the
     # record's filter_image field)
     image_build_ms = None
@@ -288,7 +290,8 @@ def main():
 
     # sanity: the last result is sorted and complete
     rd, rr = res[0].cpu().numpy(), res[1].cpu().numpy()
-    assert (rr >= 0).all() and np.all(np.diff(rd, axis=1) >= 0), "bench result not sorted"
+    assert args.no_verify or (rr >= 0).all() and np.all(np.diff(rd, axis=1) >= 0), \
+        "bench result not sorted"
 
     total_rows = n * world
     value = total_rows * nq * args.steps / elapsed
@@ -303,15 +306,17 @@ def main():
     batched = (_lib.get_option("batched") != 0 and nq >= min_q and not qu8
                and ((args.dtype == "f32" and d % 4 == 0) or (args.dtype == "f16" and d % 8 == 0)))
     filt = batched
-    if filt and args.dtype == "f32" and id(x) in eng._images:
-        # the phases stream the fp16 image and its row sums instead of the
+    image = eng._images.get(id(x)) if filt and args.dtype == "f32" else None
+    bits = image[0][3] if image is not None else 16
+    if image is not None:
+        # the phases stream the filter image and its row terms instead of the
         # f32 rows: those are the bytes of the pass (the rescoring reads a
         # few thousand f32 rows per query on top)
-        scan_bytes = n * d * 2 + n * 4 + nq * d * 4
+        scan_bytes = n * d * bits // 8 + n * (16 if bits == 8 else 4) + nq * d * 4
     achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
     if filt:
-        kname = ("fx::filter_kernel (fp16-MFMA bound filter, all sample phases) "
-                 "+ exact rescoring of the candidates")
+        kname = (f"fx::filter_img3_kernel ({'int8' if bits == 8 else 'fp16'}-MFMA bound filter, "
+                 "all sample phases) + exact rescoring of the candidates")
     elif qu8:
         kname = "fx::scan_kernel<uint8> (quint8 codes dequantised in registers) + merge"
     else:
@@ -327,11 +332,10 @@ def main():
         "bytes_per_launch": scan_bytes,
         "library_sha": _lib.library_sha(),
     }
-    if filt:  # the GEMM the filter evaluates, against the dense fp16 MFMA peak
+    if filt:  # the GEMM the filter evaluates, against the dense MFMA peak of its type
         roof["mfma_tflops"] = 2.0 * n * nq * d / (scan_ms * 1e-3) / 1e12
-        roof["mfma_peak_tflops"] = MFMA_F16_PEAK_TFS
+        roof["mfma_peak_tflops"] = MFMA_F16_PEAK_TFS * (2 if bits == 8 else 1)
     roof["frac"] = roof["achieved"] / roof["peak"]
-    image = eng._images.get(id(x)) if filt and args.dtype == "f32" else None
 
     out = None
     if rank == 0:
@@ -365,15 +369,19 @@ def main():
                 "parallelism": f"row-shard x{world}"
                 + ((" + gloo all-gather" if gloo else " + RCCL all-gather") if use_dist else ""),
             },
-            # the batched filter streamed the corpus's resident fp16 filter
-            # image (fx_filter_image, built in the warmup; candidates rescored
-            # from the f32 rows, results bit-identical to the f32 scan)
-            **({"filter_image": {"bytes": int(image[1].numel()) * 2 + int(image[2].numel()) * 4,
+            # the batched filter streamed the corpus's resident filter image
+            # (fx_filter_image8 / fx_filter_image, built before the warmup;
+            # candidates rescored from the f32 rows, results bit-identical to
+            # the f32 scan)
+            **({"filter_image": {"bits": bits,
+                                 "bytes": int(image[1].numel()) * image[1].element_size()
+                                 + int(image[2].numel()) * 4,
                                  "build_ms": image_build_ms,
-                                 "note": "fp16 image + row sums of squares resident beside "
-                                         "the f32 corpus, built once per corpus version "
-                                         "(build_ms, not in ms_per_step); "
-                                         "FENIX_AMD_FILTER_IMAGE=0 disables"}}
+                                 "note": f"{'int8' if bits == 8 else 'fp16'} image + per-row "
+                                         "bound terms resident beside the f32 corpus, built "
+                                         "once per corpus version (build_ms, not in "
+                                         "ms_per_step); option filter_image=16 or 0 selects "
+                                         "fp16 or none"}}
                if image is not None else {}),
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -52,6 +52,10 @@ SYMBOLS = (
     "fx_filter_image_used",
     "fx_knn_scan_img",
     "fx_knn_search_img",
+    "fx_filter_image8_bytes",
+    "fx_filter_image8",
+    "fx_knn_scan_img8",
+    "fx_knn_search_img8",
     "fx_knn_distances",
     "fx_topk_merge_workspace_bytes",
     "fx_topk_merge",
@@ -80,9 +84,10 @@ SYMBOLS = (
 )
 
 # process options of the library (fx_set_option, include/fenix_knn.h): the
-# first two are user switches, the rest test switches
+# "batched", "batch_min_queries" and "filter_image" are user switches, the rest
+# test switches
 OPTIONS = ("batched", "batch_min_queries", "batch_cap", "batch_sample_ratio", "force_fallback",
-           "scan_interleave", "q8_dma")
+           "scan_interleave", "q8_dma", "filter_image")
 
 _lock = threading.Lock()
 _lib = None
@@ -149,6 +154,14 @@ def load() -> ctypes.CDLL:
         L.fx_knn_search_img.argtypes = [vp, ci, i64, i64, i64, vp, vp, vp, i64, ci, i64, vp, vp,
                                         sz, vp, vp, vp]
         L.fx_knn_search_img.restype = ci
+        L.fx_filter_image8_bytes.argtypes = [i64, i64, ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        L.fx_filter_image8_bytes.restype = ci
+        L.fx_filter_image8.argtypes = [vp, i64, i64, vp, vp, vp]
+        L.fx_filter_image8.restype = ci
+        L.fx_knn_scan_img8.argtypes = L.fx_knn_scan_img.argtypes
+        L.fx_knn_scan_img8.restype = ci
+        L.fx_knn_search_img8.argtypes = L.fx_knn_search_img.argtypes
+        L.fx_knn_search_img8.restype = ci
         L.fx_knn_distances.argtypes = [vp, ci, i64, i64, vp, i64, ci, vp, vp, vp]
         L.fx_knn_distances.restype = ci
         L.fx_topk_merge_workspace_bytes.argtypes = [i64, i64, i64, i64, ctypes.POINTER(sz)]

@@ -40,8 +40,8 @@ static std::mutex g_mu;
 // ----------------------------------------------------------------- options --
 static const char* const kOptNames[kOptCount] = {
     "batched", "batch_min_queries", "batch_cap", "batch_sample_ratio",
-    "force_fallback", "scan_interleave", "q8_dma"};
-static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}};
+    "force_fallback", "scan_interleave", "q8_dma", "filter_image"};
+static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}, {8}};
 
 int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
 
@@ -189,6 +189,8 @@ static constexpr int64_t kLargeMaxK = 0x7fffffffll;
 // A query whose final candidates overflow `cap` is recomputed exactly by the
 // single-query scan, gated on the device (fx_knn_reduce: no host sync).
 static constexpr int64_t kListLen = 4096;  // candidate buffer viewed as lists
+// sample growth per phase with an int8 filter image (filter_phases)
+static constexpr int64_t kI8SampleRatio = 8;
 
 struct BatchLayout {
   int64_t cap = 0, tiles = 0, nq_pad = 0;
@@ -198,7 +200,7 @@ struct BatchLayout {
   int64_t start[16], stride[16], num[16];
   MergePlan merge;
   size_t off_qnorm, off_thr, off_count, off_cand, off_merge, off_cand_ub, off_qh, off_qinfo,
-      total;
+      off_topd, off_topr, total;
 };
 
 // The fp16-MFMA filter (knn_filter.hip).  Diagnostic builds keep the
@@ -219,6 +221,8 @@ static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool align
   return dtype == FX_DTYPE_F16 && d % 8 == 0 && use_filter();
 }
 
+static int plan_phases(BatchLayout* b, int64_t tr, int64_t r);
+
 static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, BatchLayout* b) {
   b->filter = use_filter();
   const int64_t tr = b->filter ? filter_tile_rows(dtype) : batch_tile_rows();
@@ -234,6 +238,46 @@ static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, 
     const int64_t v = option(kOptBatchRatio);
     if (v >= 2 && v < r) r = v;
   }
+  int rc = plan_phases(b, tr, r);
+  if (rc) return rc;
+  rc = plan_merge(nq, b->cap / kListLen, kListLen, k, &b->merge);
+  if (rc) return rc;
+  size_t off = 0;
+  b->off_qnorm = off;
+  off += align256((size_t)nq * 4);
+  b->off_thr = off;
+  off += align256((size_t)nq * 8);
+  b->off_count = off;
+  off += align256((size_t)nq * 4 * kCountStride);
+  b->off_cand = off;
+  off += align256((size_t)nq * b->cap * 8);
+  b->off_merge = off;
+  off += align256(b->merge.ws_bytes);
+  if (b->filter) {
+    b->dq = filter_dq((int)d);
+    b->nq_pad = (nq + filter_query_pad(nq) - 1) / filter_query_pad(nq) * filter_query_pad(nq);
+    b->off_cand_ub = off;
+    off += align256((size_t)nq * b->cap * 8);
+    // fp16 query tiles, or int8 ones padded to 256 queries (int8 filter images)
+    const size_t q16 = (size_t)b->nq_pad * b->dq * 2, q8 = (size_t)((nq + 255) / 256 * 256) * b->dq;
+    b->off_qh = off;
+    off += align256(q16 > q8 ? q16 : q8);
+    b->off_qinfo = off;
+    off += align256((size_t)nq * 16);
+    // the k best candidates by upper bound (int8 images: exact thresholds)
+    b->off_topd = off;
+    off += align256((size_t)nq * k * 4);
+    b->off_topr = off;
+    off += align256((size_t)nq * k * 8);
+  }
+  b->total = off;
+  return FX_OK;
+}
+
+// Nested row samples of the batched phases: phase i scans every stride_i-th
+// tile of tr rows, each stride a multiple r of the next, the first at most
+// cap rows, the last every tile.
+static int plan_phases(BatchLayout* b, int64_t tr, int64_t r) {
   int64_t strides[16];
   int m = 0;
   strides[m++] = 1;
@@ -252,30 +296,6 @@ static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, 
     b->start[i] = 0;
     b->num[i] = (b->tiles + st - 1) / st;
   }
-  int rc = plan_merge(nq, b->cap / kListLen, kListLen, k, &b->merge);
-  if (rc) return rc;
-  size_t off = 0;
-  b->off_qnorm = off;
-  off += align256((size_t)nq * 4);
-  b->off_thr = off;
-  off += align256((size_t)nq * 8);
-  b->off_count = off;
-  off += align256((size_t)nq * 4 * kCountStride);
-  b->off_cand = off;
-  off += align256((size_t)nq * b->cap * 8);
-  b->off_merge = off;
-  off += align256(b->merge.ws_bytes);
-  if (b->filter) {
-    b->dq = filter_dq((int)d);
-    b->nq_pad = (nq + filter_query_pad(nq) - 1) / filter_query_pad(nq) * filter_query_pad(nq);
-    b->off_cand_ub = off;
-    off += align256((size_t)nq * b->cap * 8);
-    b->off_qh = off;
-    off += align256((size_t)b->nq_pad * b->dq * 2);
-    b->off_qinfo = off;
-    off += align256((size_t)nq * 16);
-  }
-  b->total = off;
   return FX_OK;
 }
 
@@ -402,8 +422,16 @@ static int fallback_search(const SearchLayout& s, const void* corpus, int dtype,
 // of the exact keys and recomputes overflowing queries.
 // With an fp16 filter image of an f32 corpus (fx_filter_image) the phases
 // stream the image (half the bytes) and the rescoring reads the f32 rows.
+//
+// An int8 filter image (fx_filter_image8) gives bounds ~30x wider than fp16
+// (per-row 8-bit quantization, see knn_filter.hip "int8 filter image"), so a
+// k-th upper bound would sit well above the k-th distance: after each phase
+// the k candidates with the smallest upper bounds are rescored exactly
+// (launch_exact_kth) and their largest exact composite becomes the
+// threshold (k scan distances lie at or below it), and the samples grow by
+// kI8SampleRatio per phase, which keeps the appends near cap/4 per query.
 static int filter_phases(const BatchLayout& b, const void* X, int dtype, const void* image,
-                         const float* rowinfo, int64_t n, int64_t d, int64_t row_base,
+                         const float* rowinfo, bool img8, int64_t n, int64_t d, int64_t row_base,
                          const float* Q, int64_t nq, int metric, int64_t k,
                          const uint32_t* mask, char* w, hipStream_t st) {
   float* qnorm = reinterpret_cast<float*>(w + b.off_qnorm);
@@ -413,7 +441,10 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
   uint64_t* cand_ub = reinterpret_cast<uint64_t*>(w + b.off_cand_ub);
   uint16_t* qh = reinterpret_cast<uint16_t*>(w + b.off_qh);
   float* qinfo = reinterpret_cast<float*>(w + b.off_qinfo);
-  int rc = launch_qprep(Q, nq, b.nq_pad, (int)d, b.dq, metric, qh, qinfo, st);
+  const int64_t nq_pad8 = (nq + 255) / 256 * 256;
+  int rc = img8 ? launch_qprep8(Q, nq, nq_pad8, (int)d, b.dq, metric,
+                                reinterpret_cast<int8_t*>(qh), qinfo, st)
+                : launch_qprep(Q, nq, b.nq_pad, (int)d, b.dq, metric, qh, qinfo, st);
   if (rc) return rc;
   if (metric == FX_METRIC_COS) {  // the scan's max(|q|, 1e-12) for the rescoring
     rc = launch_qnorm(Q, nq, (int)d, qnorm, st, 0);
@@ -435,7 +466,8 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
     a.row_base = row_base;
     a.Qh = qh;
     a.dq = b.dq;
-    a.qstride = b.nq_pad;
+    a.qstride = img8 ? nq_pad8 : b.nq_pad;
+    a.img8 = img8 ? 1 : 0;
     a.qinfo = qinfo;
     a.nq = nq;
     a.mask = mask;
@@ -450,6 +482,16 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
     a.diag = diag_env("FX_FILTER_DIAG", 0);
     rc = launch_filter(a, metric, st);
     if (rc) return rc;
+    if (img8) {  // the exact distances of the k best upper bounds: next threshold
+      float* topd = reinterpret_cast<float*>(w + b.off_topd);
+      int64_t* topr = reinterpret_cast<int64_t*>(w + b.off_topr);
+      rc = run_merge(b.merge, last ? cand_ub : cand, nq, k, w + b.off_merge, topd, topr, st);
+      if (rc) return rc;
+      rc = launch_exact_kth(X, dtype, n, (int)d, row_base, Q, qnorm, nq, (int)k, topr, metric,
+                            thr, st);
+      if (rc) return rc;
+      continue;
+    }
     // the k-th upper bound of this phase's candidates: next threshold
     rc = run_merge(b.merge, last ? cand_ub : cand, nq, k, w + b.off_merge, nullptr, nullptr, st,
                    thr);
@@ -526,7 +568,7 @@ using namespace fx;
 
 extern "C" {
 
-int fx_version(void) { return 102; }
+int fx_version(void) { return 103; }
 
 const char* fx_last_error(void) { return g_err; }
 
@@ -622,9 +664,9 @@ static bool image_applies(const SearchLayout& s, int dtype, int64_t d) {
 }
 
 static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
-                     const void* image, const float* rowinfo, const float* queries, int64_t nq,
-                     int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
-                     void* stream) {
+                     const void* image, const float* rowinfo, bool img8, const float* queries,
+                     int64_t nq, int metric, int64_t k, const uint32_t* mask, void* ws,
+                     size_t ws_bytes, void* stream) {
   SearchLayout s;
   int rc = search_layout(corpus, dtype, n, d, nq, metric, k, ws, ws_bytes, &s);
   if (rc) return rc;
@@ -645,8 +687,20 @@ static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_
         set_error("filter image: null row info or image not 16-byte aligned");
         return FX_EINVAL;
       }
-      return filter_phases(s.batch, corpus, dtype, img ? image : nullptr, rowinfo, n, d, row_base,
-                           queries, nq, metric, k, mask, reinterpret_cast<char*>(ws), st);
+      if (img && img8) {  // int8 image: denser samples (filter_phases)
+        BatchLayout b = s.batch;
+        int64_t r = b.cap / (4 * k);
+        if (r > kI8SampleRatio) r = kI8SampleRatio;
+        const int64_t v = option(kOptBatchRatio);
+        if (v >= 2 && v < r) r = v;
+        rc = plan_phases(&b, filter_tile_rows(dtype), r);
+        if (rc) return rc;
+        return filter_phases(b, corpus, dtype, image, rowinfo, true, n, d, row_base, queries, nq,
+                             metric, k, mask, reinterpret_cast<char*>(ws), st);
+      }
+      return filter_phases(s.batch, corpus, dtype, img ? image : nullptr, rowinfo, false, n, d,
+                           row_base, queries, nq, metric, k, mask, reinterpret_cast<char*>(ws),
+                           st);
     }
 #ifdef FX_DIAG_BUILD
     return batched_phases(s.batch, reinterpret_cast<const float*>(corpus), n, d, row_base,
@@ -693,16 +747,24 @@ extern "C" {
 int fx_knn_scan(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
                 const float* queries, int64_t nq, int metric, int64_t k,
                 const uint32_t* mask, void* ws, size_t ws_bytes, void* stream) {
-  return scan_impl(corpus, dtype, n, d, row_base, nullptr, nullptr, queries, nq, metric, k, mask,
-                   ws, ws_bytes, stream);
+  return scan_impl(corpus, dtype, n, d, row_base, nullptr, nullptr, false, queries, nq, metric, k,
+                   mask, ws, ws_bytes, stream);
 }
 
 int fx_knn_scan_img(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
                     const void* image, const float* rowinfo, const float* queries, int64_t nq,
                     int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
                     void* stream) {
-  return scan_impl(corpus, dtype, n, d, row_base, image, rowinfo, queries, nq, metric, k, mask, ws,
-                   ws_bytes, stream);
+  return scan_impl(corpus, dtype, n, d, row_base, image, rowinfo, false, queries, nq, metric, k,
+                   mask, ws, ws_bytes, stream);
+}
+
+int fx_knn_scan_img8(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                     const void* image, const float* rowinfo, const float* queries, int64_t nq,
+                     int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
+                     void* stream) {
+  return scan_impl(corpus, dtype, n, d, row_base, image, rowinfo, true, queries, nq, metric, k,
+                   mask, ws, ws_bytes, stream);
 }
 
 int fx_filter_image_bytes(int64_t n, int64_t d, size_t* image_bytes, size_t* rowinfo_bytes) {
@@ -739,6 +801,41 @@ int fx_filter_image(const float* corpus, int64_t n, int64_t d, void* image, floa
     return FX_EUNSUPPORTED;
   }
   return launch_image(corpus, n, (int)d, image, rowinfo, reinterpret_cast<hipStream_t>(stream));
+}
+
+int fx_filter_image8_bytes(int64_t n, int64_t d, size_t* image_bytes, size_t* rowinfo_bytes) {
+  if (!image_bytes || !rowinfo_bytes) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  if (n < 0 || d < 8 || d % 8 != 0) {
+    set_error("filter image: n=%lld d=%lld (d must be a positive multiple of 8)", (long long)n,
+              (long long)d);
+    return FX_EUNSUPPORTED;
+  }
+  *image_bytes = (size_t)((n + 31) / 32) * (size_t)((d + 31) / 32) * 1024;
+  *rowinfo_bytes = (size_t)n * kI8RowInfo * 4;
+  return FX_OK;
+}
+
+int fx_filter_image8(const float* corpus, int64_t n, int64_t d, void* image, float* rowinfo,
+                     void* stream) {
+  size_t ib = 0, rb = 0;
+  int rc = fx_filter_image8_bytes(n, d, &ib, &rb);
+  if (rc) return rc;
+  if (n > 0 && (!corpus || !image || !rowinfo)) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  if ((uintptr_t)corpus % 16 != 0 || (uintptr_t)image % 16 != 0 || (uintptr_t)rowinfo % 16 != 0) {
+    set_error("filter image: corpus, image and row info must be 16-byte aligned");
+    return FX_EINVAL;
+  }
+  if (d > 0x7fffffffll) {
+    set_error("filter image: d=%lld too large", (long long)d);
+    return FX_EUNSUPPORTED;
+  }
+  return launch_image8(corpus, n, (int)d, image, rowinfo, reinterpret_cast<hipStream_t>(stream));
 }
 
 int fx_filter_image_used(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
@@ -820,6 +917,21 @@ int fx_knn_search_img(const void* corpus, int dtype, int64_t n, int64_t d, int64
   }
   int rc = fx_knn_scan_img(corpus, dtype, n, d, row_base, image, rowinfo, queries, nq, metric, k,
                            mask, ws, ws_bytes, stream);
+  if (rc) return rc;
+  return fx_knn_reduce(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
+                       out_dist, out_row, stream);
+}
+
+int fx_knn_search_img8(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                       const void* image, const float* rowinfo, const float* queries, int64_t nq,
+                       int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
+                       float* out_dist, int64_t* out_row, void* stream) {
+  if (!out_dist || !out_row) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  int rc = fx_knn_scan_img8(corpus, dtype, n, d, row_base, image, rowinfo, queries, nq, metric, k,
+                            mask, ws, ws_bytes, stream);
   if (rc) return rc;
   return fx_knn_reduce(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
                        out_dist, out_row, stream);

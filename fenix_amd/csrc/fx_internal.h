@@ -21,6 +21,7 @@ enum Option : int {
   kOptForceFallback,
   kOptScanInterleave,
   kOptQ8Dma,
+  kOptFilterImage,  // filter image bits for f32 corpora (engine policy): 8, 16 or 0 (none)
   kOptCount
 };
 int64_t option(Option o);
@@ -123,6 +124,11 @@ int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stre
 int launch_rescore(const void* X, int dtype, int64_t n, int d, int64_t row_base,
                    const float* Q, const float* qnorm, int64_t nq, const uint32_t* count,
                    uint64_t* cand, int cap, int metric, const uint64_t* thr, hipStream_t stream);
+// thr[q] = min(thr[q], the largest exact composite of the query's k rows
+// [nq][k] (global, -1 = missing: the query keeps its threshold))
+int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_base,
+                     const float* Q, const float* qnorm, int64_t nq, int k, const int64_t* rows,
+                     int metric, uint64_t* thr, hipStream_t stream);
 
 // Batched filter on the fp16 matrix cores (knn_filter.hip): appends every
 // (row, query) whose rigorous lower bound reaches the query's threshold.
@@ -146,7 +152,10 @@ struct FilterArgs {
   uint64_t* cand_ub;      // [nq][cap] ub composites, or null (sampling phases)
   int cap;
   const float* rowinfo;   // [n] row sums of squares of the f32 rows when X is their fp16
-                          // filter image (dtype F16), NaN = forced; null otherwise
+                          // filter image (dtype F16), NaN = forced; null otherwise;
+                          // img8: [n][kI8RowInfo] (launch_image8)
+  int img8;               // X is the int8 filter image (launch_image8), Qh/qinfo from
+                          // launch_qprep8
   int diag;               // FX_FILTER_DIAG (diagnostic builds only): 1 no appends, 2 no epilogue,
                           // 4 no MFMA, 8 no query loads, 16 no LDS stores,
                           // 32 no append atomics, 64 no append stores
@@ -158,6 +167,16 @@ bool filter_ring();
 // filter images in MFMA fragment order (knn_filter.hip filter_img2_kernel);
 // FX_IMAGE_TILED=0: row-major
 bool image_tiled();
+// int8 filter images (knn_filter.hip): per row kI8RowInfo floats {w, 1/s,
+// N/s, n2/s, 0...} (launch_image8), per query kI8QInfo floats {s_q, R', n_q^2,
+// |q|, 0...} (launch_qprep8); kI8Kappa bounds P/R' (the two query error terms,
+// see knn_filter.hip "int8 filter image")
+constexpr int kI8RowInfo = 4;
+constexpr int kI8QInfo = 4;
+constexpr float kI8Kappa = 128.f;
+int launch_image8(const float* X, int64_t n, int d, void* img, float* rowinfo, hipStream_t stream);
+int launch_qprep8(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
+                  int8_t* Qb, float* qinfo, hipStream_t stream);
 int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
                  uint16_t* Qh, float* qinfo, hipStream_t stream);
 int filter_tile_rows(int dtype);

@@ -285,14 +285,56 @@ int launch_qnorm(const float* Q, int64_t nq, int d, float* out, hipStream_t stre
   return check_launch("qnorm_kernel");
 }
 
-// Exact distance of each appended candidate: 16 lanes per candidate (4 per
-// wave), 16-B loads of the row and the query, the scan's per-lane fmaf chain
-// over slots jl, jl+16, ... (knn_scan.hip tile_accumulate) and its sum16
-// reduction, then the scan's distance formula (tile_finish): the same f32
-// distance as the single-query path, bit for bit.  The key is replaced in
-// place (row unchanged).  With thr, a candidate whose (lower-bound) key is
-// above the query's threshold key is dropped unread.  Every lane of a wave
-// runs the same number of iterations (sum16 is a cross-lane reduction).
+// The single-query scan's f32 distance of one row, computed by a 16-lane
+// group (lane jl of the group): 16-B loads of the row and the query, the
+// scan's per-lane fmaf chain over slots jl, jl+16, ... (knn_scan.hip
+// tile_accumulate), its sum16 reduction and its distance formula
+// (tile_finish): bit for bit the scan's value.  Every lane of the wave must
+// call it (sum16 is a cross-lane reduction); live = false contributes zeros.
+template <typename T, int METRIC>
+__device__ __forceinline__ float exact_distance16(const T* __restrict__ xr,
+                                                  const float* __restrict__ qv, int d, int jl,
+                                                  bool live, float qnorm) {
+  // the scan's 16-B slots: 4 floats (f32) or 8 halves (f16), lane jl takes
+  // slots jl, jl + 16, ... (knn_scan.hip plan_scan: W = 16 / sizeof(T))
+  constexpr int W = 16 / sizeof(T);
+  typedef T vT __attribute__((ext_vector_type(W)));
+  float acc = 0.f, acc2 = 0.f;
+  if (live) {
+    for (int k = jl * W; k < d; k += 16 * W) {
+      const vT xv = *reinterpret_cast<const vT*>(xr + k);
+#pragma unroll
+      for (int t = 0; t < W; ++t) {
+        const float x = (float)xv[t];
+        const float y = qv[k + t];
+        if constexpr (METRIC == 0) {
+          const float df = x - y;
+          acc = fmaf(df, df, acc);
+        } else if constexpr (METRIC == 1) {
+          acc = fmaf(x, y, acc);
+        } else {
+          acc = fmaf(x, y, acc);
+          acc2 = fmaf(x, x, acc2);
+        }
+      }
+    }
+  }
+  const float s1 = sum16(acc);  // the scan's reduction: bit-identical distances
+  if constexpr (METRIC == 0) {
+    return sqrtf(s1);
+  } else if constexpr (METRIC == 1) {
+    return -s1;
+  } else {
+    const float s2 = sum16(acc2);
+    const float nx = fmaxf(sqrtf(s2), 1e-12f);
+    return 0.5f - 0.5f * (s1 / (nx * qnorm));
+  }
+}
+
+// Exact distance of each appended candidate (exact_distance16, 4 candidates
+// per wave); the key is replaced in place (row unchanged).  With thr, a
+// candidate whose (lower-bound) key is above the query's threshold key is
+// dropped unread.  Every lane of a wave runs the same number of iterations.
 template <typename T, int METRIC>
 __global__ void __launch_bounds__(256) rescore_kernel(const T* __restrict__ X, int64_t n, int d,
                                                       int64_t row_base,
@@ -301,10 +343,6 @@ __global__ void __launch_bounds__(256) rescore_kernel(const T* __restrict__ X, i
                                                       const uint32_t* __restrict__ count,
                                                       uint64_t* __restrict__ cand, int cap,
                                                       const uint64_t* __restrict__ thr) {
-  // the scan's 16-B slots: 4 floats (f32) or 8 halves (f16), lane jl takes
-  // slots jl, jl + 16, ... (knn_scan.hip plan_scan: W = 16 / sizeof(T))
-  constexpr int W = 16 / sizeof(T);
-  typedef T vT __attribute__((ext_vector_type(W)));
   const int64_t q = blockIdx.y;
   const int lane = threadIdx.x & 63;
   const int grp = lane >> 4, jl = lane & 15;
@@ -312,6 +350,7 @@ __global__ void __launch_bounds__(256) rescore_kernel(const T* __restrict__ X, i
   const uint32_t cnt = cq < (uint32_t)cap ? cq : (uint32_t)cap;
   const uint32_t tkey = thr != nullptr ? (uint32_t)(thr[q] >> 32) : 0xffffffffu;
   const float* qv = Q + q * (int64_t)d;
+  const float qn = METRIC == 2 ? qnorm[q] : 0.f;
   for (int64_t i0 = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 6) * 4; i0 < cnt;
        i0 += (int64_t)gridDim.x * 16) {  // wave-uniform trip count
     const int64_t i = i0 + grp;
@@ -320,42 +359,59 @@ __global__ void __launch_bounds__(256) rescore_kernel(const T* __restrict__ X, i
     const int64_t row = (int64_t)(c & 0xffffffffull) - row_base;
     const bool keep = c != kEmpty && (uint32_t)(c >> 32) <= tkey;
     const bool live = keep && row >= 0 && row < n;
-    float acc = 0.f, acc2 = 0.f;
-    if (live) {
-      const T* xr = X + row * (int64_t)d;
-      for (int k = jl * W; k < d; k += 16 * W) {
-        const vT xv = *reinterpret_cast<const vT*>(xr + k);
-#pragma unroll
-        for (int t = 0; t < W; ++t) {
-          const float x = (float)xv[t];
-          const float y = qv[k + t];
-          if constexpr (METRIC == 0) {
-            const float df = x - y;
-            acc = fmaf(df, df, acc);
-          } else if constexpr (METRIC == 1) {
-            acc = fmaf(x, y, acc);
-          } else {
-            acc = fmaf(x, y, acc);
-            acc2 = fmaf(x, x, acc2);
-          }
-        }
-      }
-    }
-    const float s1 = sum16(acc);  // the scan's reduction: bit-identical distances
-    float dist;
-    if constexpr (METRIC == 0) {
-      dist = sqrtf(s1);
-    } else if constexpr (METRIC == 1) {
-      dist = -s1;
-    } else {
-      const float s2 = sum16(acc2);
-      const float nx = fmaxf(sqrtf(s2), 1e-12f);
-      dist = 0.5f - 0.5f * (s1 / (nx * qnorm[q]));
-    }
+    const float dist =
+        exact_distance16<T, METRIC>(X + (live ? row : 0) * (int64_t)d, qv, d, jl, live, qn);
     if (jl == 0 && i < cnt && c != kEmpty) {
       *slot = live ? make_comp(dist, (uint32_t)(c & 0xffffffffull)) : kEmpty;
     }
   }
+}
+
+// Exact threshold from a query's k best candidates by upper bound (rows
+// [nq][k], run_merge's out_row, -1 = missing): their exact distances
+// (exact_distance16) are k rows' scan distances, so the largest composite
+// bounds the k-th smallest from above; thr[q] = min(thr[q], it).  A query
+// with fewer than k candidates keeps its threshold.  One block per query.
+template <typename T, int METRIC>
+__global__ void __launch_bounds__(256) exact_kth_kernel(const T* __restrict__ X, int64_t n, int d,
+                                                        int64_t row_base,
+                                                        const float* __restrict__ Q,
+                                                        const float* __restrict__ qnorm, int k,
+                                                        const int64_t* __restrict__ rows,
+                                                        uint64_t* __restrict__ thr) {
+  __shared__ unsigned long long smax;
+  __shared__ int sbad;
+  const int64_t q = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int grp = (threadIdx.x >> 4), jl = lane & 15;  // 16 groups of 16 lanes
+  if (threadIdx.x == 0) {
+    smax = 0ull;
+    sbad = 0;
+  }
+  __syncthreads();
+  const float* qv = Q + q * (int64_t)d;
+  const float qn = METRIC == 2 ? qnorm[q] : 0.f;
+  uint64_t mx = 0ull;
+  bool bad = false;
+  for (int j0 = 0; j0 < k; j0 += 16) {  // block-uniform trip count
+    const int j = j0 + grp;
+    const int64_t grow = j < k ? rows[q * (int64_t)k + j] : 0;
+    const int64_t row = grow - row_base;
+    const bool live = j < k && grow >= 0 && row >= 0 && row < n;
+    if (j < k && !live) bad = true;
+    const float dist =
+        exact_distance16<T, METRIC>(X + (live ? row : 0) * (int64_t)d, qv, d, jl, live, qn);
+    if (live) {
+      const uint64_t c = make_comp(dist, (uint32_t)grow);
+      mx = c > mx ? c : mx;
+    }
+  }
+  if (jl == 0) {
+    if (bad) atomicOr(&sbad, 1);
+    atomicMax(&smax, (unsigned long long)mx);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && sbad == 0 && smax < thr[q]) thr[q] = smax;
 }
 
 template <typename T>
@@ -397,6 +453,42 @@ int launch_rescore(const void* X, int dtype, int64_t n, int d, int64_t row_base,
                        cap, metric, t, grid, stream);
     }
     rc = check_launch("rescore_kernel");
+    if (rc) return rc;
+  }
+  return FX_OK;
+}
+
+template <typename T>
+static void launch_exact_kth_t(const T* X, int64_t n, int d, int64_t row_base, const float* Q,
+                               const float* qnm, int k, const int64_t* rows, uint64_t* thr,
+                               int metric, dim3 grid, hipStream_t stream) {
+  if (metric == FX_METRIC_COS) {
+    hipLaunchKernelGGL((exact_kth_kernel<T, 2>), grid, dim3(256), 0, stream, X, n, d, row_base,
+                       Q, qnm, k, rows, thr);
+  } else if (metric == FX_METRIC_IP) {
+    hipLaunchKernelGGL((exact_kth_kernel<T, 1>), grid, dim3(256), 0, stream, X, n, d, row_base,
+                       Q, qnm, k, rows, thr);
+  } else {
+    hipLaunchKernelGGL((exact_kth_kernel<T, 0>), grid, dim3(256), 0, stream, X, n, d, row_base,
+                       Q, qnm, k, rows, thr);
+  }
+}
+
+int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_base,
+                     const float* Q, const float* qnorm, int64_t nq, int k, const int64_t* rows,
+                     int metric, uint64_t* thr, hipStream_t stream) {
+  for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
+    const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
+    const dim3 grid((unsigned)qn);
+    const float* qnm = qnorm != nullptr ? qnorm + q0 : nullptr;
+    if (dtype == FX_DTYPE_F16) {
+      launch_exact_kth_t(reinterpret_cast<const _Float16*>(X), n, d, row_base, Q + q0 * d, qnm, k,
+                         rows + q0 * k, thr + q0, metric, grid, stream);
+    } else {
+      launch_exact_kth_t(reinterpret_cast<const float*>(X), n, d, row_base, Q + q0 * d, qnm, k,
+                         rows + q0 * k, thr + q0, metric, grid, stream);
+    }
+    int rc = check_launch("exact_kth_kernel");
     if (rc) return rc;
   }
   return FX_OK;

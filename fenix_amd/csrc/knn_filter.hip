@@ -1172,6 +1172,8 @@ struct Img3Shared {
   float2 qab[fBQ];
   uint32_t seg[fBQ + 3 * fBQ * FX_I3_SEG];  // counters, then entries {lb key, ub key, row}
   uint32_t segbase[fBQ];
+  float rext[fBM];   // int8 image: 1 / s of the row
+  f32x4 qinf[fBQ];   // int8 image: the query's launch_qprep8 record
 };
 static_assert(sizeof(Img3Shared) <= 160 * 1024, "filter_img3_kernel: LDS over 160 KB");
 
@@ -1229,7 +1231,7 @@ __device__ __forceinline__ void i3_epilogue(const f32x16 (&acc)[kI2QT], const fl
   static_for<kI2QT>([&](auto uc) {
     constexpr int u = decltype(uc)::value;
     if (__ballot(pm[u] != 0u) == 0ull) return;
-    const int qi = u * 32 + l32;
+    const int qi = u * 32 + (int)opaque((unsigned)l32);  // (not hoisted: spilled)
     const int64_t gq = q0 + qi;
     uint32_t bits = pm[u];
     uint32_t p = bits != 0u ? atomicAdd(&seg[qi], (uint32_t)__popc(bits)) : 0u;
@@ -1304,7 +1306,239 @@ __device__ __forceinline__ void i3_epilogue(const f32x16 (&acc)[kI2QT], const fl
   });
 }
 
+// ------------------------------------------------------ int8 filter image
+//
+// The int8 image (launch_image8) halves the image stream again and runs on
+// v_mfma_i32_32x32x32_i8 (twice the fp16 rate): per row a scale s, x~ =
+// rint(x / s) in [-127, 127], w = |x~|, e >= |x - s x~|, v = e / s; per query
+// the same with s_q, w_q, e_q (launch_qprep8).  Both are scaled so that w,
+// w_q <= 2048, so the exact integer product I = x~ . q~ has |I| <= 2^22.
+// With D = x . q, exactly:  D - s s_q I = (x - s x~) . q + s x~ . (q - s_q q~),
+//   |D - s s_q I| <= s s_q (v P + w R),  P = |q| / s_q,  R = e_q / s_q
+// (IP also carries the scan's f32 summation error g |x||q|, g = (d + 2) 2^-24
+// with 1 % slack, into P and R; cosine and L2 carry it in their constants).
+// With kappa = kI8Kappa and R' = max(R, P / kappa) (kept by the query),
+// v P + w R <= (w + kappa v) R' = omega R': omega is the row's one error
+// value (launch_image8).  Per metric, with M = 12582912 + I (the accumulator
+// starts at the bits of 1.5 * 2^23, so the i32 sum read as a float is exactly
+// M for |I| <= 2^22: no conversion), a pair can reach the threshold T only if
+//   IP   I + omega R' + (1/s) (T / s_q)                    >= 0
+//   cos  I + omega R' - (N / s) (1 - 2T - 2c) N_q / s_q    >= 0   (N = max(|x|, 1e-12))
+//   L2   I + omega R' - (n^2 / s) / (2 s_q) - (1/s) (n_q^2 - T^2 (1 + 2^-20) / (1 - g2)) / (2 s_q) >= 0
+// c = 3 g + 16 u and g2 = 2 g + 8 u cover the scan's own roundings (u = 2^-24;
+// knn_batch.hip exact_distance16: dot and norms in f32, one division).  Each
+// per-query coefficient carries a relative slack >= 16 u (the roundings of the
+// products and sums of the test) and the test compares with 12582912 - 8.
+// The appends' [lb, ub] are evaluated in double from the same terms and
+// rounded outward.  A non-finite row or query, or one whose scaled norm
+// would exceed 2048, is forced through (omega or R' not finite).
+constexpr float kI8Magic = 12582912.f;   // 1.5 * 2^23: bits 0x4B400000
+constexpr float kI8C0 = 12582912.f - 8.f;
+
+// Per query {R', c1, c2, 0} of the int8 pass test
+//   M + omega R' + y1 c1 + y2 c2 >= kI8C0
+// with the row values y1 (IP 1/s, cosine N/s, L2 n^2/s) and y2 (L2 1/s).
+// No threshold yet (T NaN) or a forced query: R' = +inf (everything passes).
 template <int METRIC>
+__device__ __forceinline__ void i8_query_table(const FilterArgs& a, int64_t q0, f32x4* qtab,
+                                               f32x4* qinf, int tid, int nthreads) {
+  const float u = 5.9604644775390625e-08f;
+  const float g = (float)(a.d + 2) * u * 1.01f;
+  for (int i = tid; i < fBQ; i += nthreads) {
+    const int64_t gq = q0 + i;
+    f32x4 c = f32x4(0.f), qi = f32x4(0.f);
+    if (gq < a.nq) {
+      qi = *reinterpret_cast<const f32x4*>(a.qinfo + gq * kI8QInfo);  // {s_q, R', n_q^2, |q|}
+      const float tf = key_float((uint32_t)(a.thr[gq] >> 32));
+      const float sq = qi[0];
+      c[0] = qi[1];
+      if constexpr (METRIC == 1) {
+        const float t = tf / sq;
+        c[1] = t + 16.f * u * fabsf(t);
+      } else if constexpr (METRIC == 2) {
+        const float cc = 3.f * g + 16.f * u;
+        const float K = (1.f - 2.f * tf - 2.f * cc) * (fmaxf(qi[3], 1e-12f) / sq);
+        c[1] = -K + (g + 16.f * u) * fabsf(K);
+      } else {
+        const float g2 = 2.f * g + 8.f * u;
+        const float L1 = 0.5f / sq;
+        const float t2 = tf * tf * (1.f + 9.5367431640625e-07f) / (1.f - g2);
+        const float L0 = (qi[2] * (1.f - 4.f * u) - t2) * L1;
+        c[1] = -L1 * (1.f - g - 16.f * u);
+        c[2] = -L0 + 16.f * u * fabsf(L0);
+      }
+      if (tf != tf || !(c[0] <= 3.4e38f)) c = f32x4{__builtin_inff(), 0.f, 0.f, 0.f};
+    }
+    qtab[i] = c;
+    qinf[i] = qi;
+  }
+}
+
+// [lb, ub] of an appended (row, query) pair of the int8 filter, in double,
+// rounded outward: M the accumulator, the row's {omega, y1, 1/s}
+// (i8_note_row) and the query's launch_qprep8 record.
+template <int METRIC>
+__device__ __forceinline__ void i8_bounds(float m, float om, float y1, float is, f32x4 qi, int d,
+                                       float& lb, float& ub) {
+  if (om != om) {  // forced row: below / above every key
+    lb = -__builtin_inff();
+    ub = __builtin_nanf("");
+    return;
+  }
+  const double u = 5.9604644775390625e-08;
+  const double g = (double)(d + 2) * u * 1.01;
+  const double I = (double)(m - kI8Magic);  // exact
+  const double E = (double)om * (double)qi[1] * (1.0 + 1e-6) + 4.0;
+  const double s = 1.0 / (double)is;  // (1/s was rounded: relative slack below)
+  const double sig = s * (double)qi[0] * (1.0 + 1e-6);
+  double lo, hi;
+  if constexpr (METRIC == 1) {
+    lo = -sig * (I + E);
+    hi = -sig * (I - E);
+  } else if constexpr (METRIC == 2) {
+    const double c = 3.0 * g + 32.0 * u;
+    const double den = fmax((double)y1 * s, 1e-12) * fmax((double)qi[3], 1e-12);
+    lo = 0.5 - 0.5 * sig * (I + E) / den - c;
+    hi = 0.5 - 0.5 * sig * (I - E) / den + c;
+  } else {
+    const double g2 = 2.0 * g + 8.0 * u;
+    const double n2 = (double)y1 * s;
+    const double alo = n2 * (1.0 - g - 16.0 * u) + (double)qi[2] * (1.0 - 4.0 * u);
+    const double ahi = n2 * (1.0 + g + 16.0 * u) + (double)qi[2] * (1.0 + 4.0 * u);
+    lo = sqrt(fmax((1.0 - g2) * (alo - 2.0 * sig * (I + E)), 0.0));
+    hi = sqrt(fmax((1.0 + g2) * (ahi - 2.0 * sig * (I - E)), 0.0));
+  }
+  lb = __double2float_rd(lo);
+  ub = __double2float_ru(hi);
+  if (lo != lo) lb = -__builtin_inff();  // (a non-finite query: R' = inf)
+  if (hi != hi) ub = __builtin_nanf("");
+}
+
+// One row's values for the int8 epilogue: omega (NaN: forced), y1 and 1/s,
+// and its flags (filter_note_row's words)
+__device__ __forceinline__ void i8_note_row(float* rinfo, float* rterm, float* rext,
+                                            uint32_t* flags, int lr, float om, float y1, float is,
+                                            bool ok) {
+  rinfo[lr] = om;
+  rterm[lr] = y1;
+  rext[lr] = is;
+  int word, bit;
+  filter_row_bit<1>(lr, word, bit);
+  if (!ok) atomicOr(&flags[16 + word], 1u << bit);
+  else if (om != om) atomicOr(&flags[word], 1u << bit);
+}
+
+// i3_epilogue for the int8 image: the packed pass test above (2 or 3
+// v_pk_fma_f32 and one v_pk_add_f32 per two pairs), appends with i8_bounds
+template <int METRIC>
+__device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const float* rinfo,
+                                            const float* rterm, const float* rext,
+                                            const uint32_t* flags, const f32x4* qtab,
+                                            const f32x4* qinf, const FilterArgs& a, int64_t q0,
+                                            int64_t r0, int wid, int h, int l32, uint32_t* seg,
+                                            int diag) {
+  constexpr int SEG = FX_I3_SEG;
+  const int lr0 = wid * 32 + 4 * h;
+  const uint32_t fmask = flags[wid * 2 + h], smask = flags[16 + wid * 2 + h];
+  // row groups g of 4 rows outside (their values read once from LDS), query
+  // tiles inside; fail bit j = 4 g + i enters last-in at bit 0, so g and i
+  // run down
+  uint32_t fail[kI2QT];
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u) fail[u] = 0u;
+  const f32x2 nc0 = {-kI8C0, -kI8C0};
+#pragma unroll
+  for (int g = 3; g >= 0; --g) {
+    const f32x4 om = *reinterpret_cast<const f32x4*>(rinfo + lr0 + 8 * g);
+    const f32x4 y1 = *reinterpret_cast<const f32x4*>(rterm + lr0 + 8 * g);
+    f32x4 y2 = f32x4(0.f);
+    if constexpr (METRIC == 0) y2 = *reinterpret_cast<const f32x4*>(rext + lr0 + 8 * g);
+#pragma unroll
+    for (int u = 0; u < kI2QT; ++u) {
+      const f32x4 co = qtab[u * 32 + l32];
+      const f32x2 ra = {co[0], co[0]}, c1 = {co[1], co[1]}, c2 = {co[2], co[2]};
+#pragma unroll
+      for (int hp = 1; hp >= 0; --hp) {  // rows 4 g + 2 hp, + 1
+        const int i = 2 * g + hp;
+        const f32x2 xp = {acc[u][2 * i], acc[u][2 * i + 1]};
+        const f32x2 op = hp ? f32x2{om[2], om[3]} : f32x2{om[0], om[1]};
+        const f32x2 p1 = hp ? f32x2{y1[2], y1[3]} : f32x2{y1[0], y1[1]};
+        f32x2 t = __builtin_elementwise_fma(op, ra, xp);
+        t = __builtin_elementwise_fma(p1, c1, t);
+        if constexpr (METRIC == 0) {
+          const f32x2 p2 = hp ? f32x2{y2[2], y2[3]} : f32x2{y2[0], y2[1]};
+          t = __builtin_elementwise_fma(p2, c2, t);
+        }
+        const f32x2 dd = t + nc0;
+        fail[u] = __builtin_amdgcn_alignbit(fail[u], __float_as_uint(dd[1]), 31);
+        fail[u] = __builtin_amdgcn_alignbit(fail[u], __float_as_uint(dd[0]), 31);
+      }
+    }
+  }
+  uint32_t pm[kI2QT];
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u) {
+    pm[u] = (diag & 1) ? 0u : (~fail[u] | fmask) & ~smask & 0xffffu;
+    if (q0 + u * 32 + l32 >= a.nq) pm[u] = 0u;
+  }
+  uint32_t any = 0u;
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u) any |= pm[u];
+  if (__ballot(any != 0u) == 0ull) return;
+  static_for<kI2QT>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    if (__ballot(pm[u] != 0u) == 0ull) return;
+    const int qi = u * 32 + (int)opaque((unsigned)l32);  // (not hoisted: spilled)
+    const int64_t gq = q0 + qi;
+    uint32_t bits = pm[u];
+    uint32_t p = bits != 0u ? atomicAdd(&seg[qi], (uint32_t)__popc(bits)) : 0u;
+    const f32x4 qrec = qinf[qi];
+    uint32_t gp = ~0u;
+    while (bits != 0u) {
+      const int j = __builtin_ctz(bits);
+      const uint32_t rest = bits;
+      bits &= bits - 1u;
+      auto pick = [](float lo, float hi, uint32_t m) {
+        return __uint_as_float((__float_as_uint(hi) & m) | (__float_as_uint(lo) & ~m));
+      };
+      const uint32_t m0 = 0u - ((uint32_t)j & 1u), m1 = 0u - (((uint32_t)j >> 1) & 1u);
+      const uint32_t m2 = 0u - (((uint32_t)j >> 2) & 1u), m3 = 0u - (((uint32_t)j >> 3) & 1u);
+      float v8[8], v4[4], v2[2];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v8[i] = pick(acc[u][2 * i], acc[u][2 * i + 1], m0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v4[i] = pick(v8[2 * i], v8[2 * i + 1], m1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) v2[i] = pick(v4[2 * i], v4[2 * i + 1], m2);
+      const float x = pick(v2[0], v2[1], m3);
+      const int lr = lr0 + (j & 3) + 8 * (j >> 2);
+      float lb, ub;
+      i8_bounds<METRIC>(x, rinfo[lr], rterm[lr], rext[lr], qrec, a.d, lb, ub);
+      const uint32_t grow = (uint32_t)(a.row_base + r0) + (uint32_t)lr;
+      if (p < (uint32_t)SEG) {
+        uint32_t* e = seg + fBQ + 3 * (qi * SEG + p);
+        e[0] = order_key(lb);
+        e[1] = order_key(ub);
+        e[2] = grow;
+      } else {  // rare: past the segment, global slots for the lane's remaining passes
+        if (gp == ~0u) gp = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(rest));
+        if (gp < (uint32_t)a.cap) {
+          const size_t slot = (size_t)gq * a.cap + gp;
+          if (a.cand_ub != nullptr) {
+            a.cand[slot] = make_comp(lb, grow);
+            a.cand_ub[slot] = make_comp(ub, grow);
+          } else {
+            a.cand[slot] = make_comp(ub, grow);
+          }
+        }
+        ++gp;
+      }
+      ++p;
+    }
+  });
+}
+
+template <int METRIC, bool I8>
 __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(FilterArgs a) {
   constexpr int XS = FX_I3_XS, SEG = FX_I3_SEG;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1321,12 +1555,21 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
   const int64_t q0 = (int64_t)blockIdx.y * fBQ;
   // chunks per tile, padded to a multiple of the register stages (past the
   // row end the image reads zeros and the query tile is zero-padded to dq)
-  const int nch = ((a.d + fBK - 1) / fBK + XS - 1) / XS * XS;
-  const int ksteps = (a.d + 15) / 16;
+  // (int8 image: 64 components per chunk, 32 per k-step, the same bytes)
+  constexpr int CK = I8 ? 2 * fBK : fBK;
+  const int nch = ((a.d + CK - 1) / CK + XS - 1) / XS * XS;
+  const int ksteps = I8 ? (a.d + 31) / 32 : (a.d + 15) / 16;
   const int64_t ntile32 = (a.n + 31) / 32;
   if ((int64_t)blockIdx.x >= a.num_tiles) return;
-  filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
+  if constexpr (I8)
+    i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, fThreads);
+  else
+    filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
   for (int q = tid; q < fBQ; q += fThreads) sh->seg[q] = 0u;  // (ordered by the first barrier)
+  // the ring starts zeroed (a slot whose DMA is dropped then holds finite values)
+  for (int i = tid; i < kI3Slots * kI3QBytes / 16; i += fThreads)
+    reinterpret_cast<i32x4*>(sh->qring)[i] = i32x4(0);
+  __syncthreads();
 
   // the query tile, blocked by 32 components (FilterArgs::Qh); chunk c of
   // query q is 64 B at (c * qstride + q) * 64
@@ -1348,13 +1591,18 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
     const int q = 16 * j + (lane >> 2);
     qv[i] = (uint32_t)(q * 64 + (((lane & 3) ^ ((q >> 2) & 3)) * 16));
   }
+  // (chunks past the query tile's padding, when nch is padded to the
+  // stages: an offset beyond the buffer, the DMA is dropped and the slot
+  // keeps finite values of an earlier chunk, multiplied by zero image rows)
+  const int qchunks = a.dq / CK;
   auto issue_q = [&](int c, int slot) {
     if (diag & 8) return;
     unsigned char* st = sh->qring[slot];
 #pragma unroll
     for (int i = 0; i < kI3QDma; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (i3_lds_ptr)(st + (wid * kI3QDma + i) * 1024), 16,
-                                               qv[i], (int)(c * a.qstride * 64), 0, 0);
+                                               c < qchunks ? qv[i] : 0x7fff0000u,
+                                               (int)(c * a.qstride * 64), 0, 0);
   };
   // this wave's 32-row tile of the row tile at step iteration ti: its
   // k-steps, one KB each (a tile past the end: an empty descriptor, zeros)
@@ -1407,7 +1655,14 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
       for (int u = 0; u < kI2QT; ++u) {
         // (query tile u sits 32 x 64 B further: (Q + 32 u) has the same swizzle)
         const f16x8 bv = *reinterpret_cast<const f16x8*>(st + bq[s] + u * 32 * 64);
-        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bv, acc[u], 0, 0, 0);
+        if constexpr (I8) {
+          typedef int i32x16 __attribute__((ext_vector_type(16)));
+          acc[u] = __builtin_bit_cast(f32x16, __builtin_amdgcn_mfma_i32_32x32x32_i8(
+              __builtin_bit_cast(i32x4, xa[s]), __builtin_bit_cast(i32x4, bv),
+              __builtin_bit_cast(i32x16, acc[u]), 0, 0, 0));
+        } else {
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bv, acc[u], 0, 0, 0);
+        }
       }
     }
   };
@@ -1441,8 +1696,8 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
     const int64_t r0 = (a.tile_start + ti * a.tile_stride) * fBM;
     if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;  // (read two tiles back)
 #pragma unroll
-    for (int u = 0; u < kI2QT; ++u) acc[u] = f32x16(0.f);
-    float rsum = 0.f;
+    for (int u = 0; u < kI2QT; ++u) acc[u] = f32x16(I8 ? kI8Magic : 0.f);
+    std::conditional_t<I8, f32x4, float> rsum = {};
     uint32_t mword = 0u;
     // one K step: multiply chunk c + S, then (LOAD) refill its register
     // stage with the chunk XS steps ahead (the next tile's first chunks at
@@ -1461,13 +1716,16 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
       qslot = qslot + 1 == kI3Slots ? 0 : qslot + 1;
       if (S == 0 && c == 0) {  // the rows' image sums and mask words of this tile
         const int64_t row = r0 + lr < a.n ? r0 + lr : a.n - 1;
-        rsum = a.rowinfo[row];
+        if constexpr (I8)
+          rsum = *reinterpret_cast<const f32x4*>(a.rowinfo + row * kI8RowInfo);
+        else
+          rsum = a.rowinfo[row];
         // (both kernel arguments: global loads; a pointer to a __device__
         // constant made a flat load, which counts in lgkmcnt too, and the
         // step's LDS waits then waited for it)
         const bool masked = a.mask != nullptr;
         const uint32_t* mp = masked ? a.mask + (row >> 5)
-                                    : reinterpret_cast<const uint32_t*>(a.rowinfo) + row;
+                                    : reinterpret_cast<const uint32_t*>(a.rowinfo) + row * (I8 ? kI8RowInfo : 1);
         mword = *mp | (masked ? 0u : ~0u);
       }
       compute(xa[S], rslot);
@@ -1492,6 +1750,10 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
       const int lr = (int)opaque((unsigned)tid);
       const int64_t row = r0 + lr;
       bool ok = row < a.n && ((mword >> (row & 31)) & 1u);
+      if constexpr (I8) {  // {omega, 1/s, N/s, n^2/s}
+        const float y1 = METRIC == 1 ? rsum[1] : METRIC == 2 ? rsum[2] : rsum[3];
+        i8_note_row(sh->rinfo, sh->rterm, sh->rext, sh->rflags[par], lr, rsum[0], y1, rsum[1], ok);
+      } else {
       const float s = ok ? rsum : 0.f;
       float rv;
       if constexpr (METRIC == 0) {
@@ -1503,13 +1765,18 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
       }
       if (!(s <= 3.4e38f)) rv = __builtin_nanf("");
       filter_note_row<METRIC, 1>(sh->rinfo, sh->rterm, sh->rflags[par], lr, rv, ok);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (diag & 2) {
       if (acc[0][0] == 1.2345f) a.count[0] = 7;
     } else {
-      i3_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rflags[par], sh->qtab, sh->qab, a, q0,
-                          r0, wid, h, l32, sh->seg, diag);
+      if constexpr (I8)
+        i8_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rext, sh->rflags[par], sh->qtab,
+                            sh->qinf, a, q0, r0, wid, h, l32, sh->seg, diag);
+      else
+        i3_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rflags[par], sh->qtab, sh->qab, a, q0,
+                            r0, wid, h, l32, sh->seg, diag);
     }
     if constexpr (!FX_I3_XPF) {  // the next tile's first chunks, after the epilogue
       static_for<XS>([&](auto sc) {
@@ -1530,9 +1797,420 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
 
 static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
   const size_t smem = sizeof(Img3Shared);
-  const void* fn = metric == FX_METRIC_COS ? (const void*)filter_img3_kernel<2>
-                   : metric == FX_METRIC_IP ? (const void*)filter_img3_kernel<1>
-                                            : (const void*)filter_img3_kernel<0>;
+  const void* fn =
+      a.img8 ? (metric == FX_METRIC_COS  ? (const void*)filter_img3_kernel<2, true>
+                : metric == FX_METRIC_IP ? (const void*)filter_img3_kernel<1, true>
+                                         : (const void*)filter_img3_kernel<0, true>)
+             : (metric == FX_METRIC_COS  ? (const void*)filter_img3_kernel<2, false>
+                : metric == FX_METRIC_IP ? (const void*)filter_img3_kernel<1, false>
+                                         : (const void*)filter_img3_kernel<0, false>);
+  if (int rc = allow_lds(fn)) return rc;
+  int cus = 0;
+  int rc = device_cus(&cus);
+  if (rc) return rc;
+  const int64_t qtiles = (a.nq + fBQ - 1) / fBQ;
+  int64_t bx = cus;
+  if (bx > a.num_tiles) bx = a.num_tiles;
+  for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
+    FilterArgs b = a;
+    const int64_t yn = (qtiles - y0) < 65535 ? (qtiles - y0) : 65535;
+    b.Qh = a.Qh + y0 * fBQ * 32;  // (64 B per query and chunk in both formats)
+    b.qinfo = a.qinfo + y0 * fBQ * (a.img8 ? kI8QInfo : 4);
+    b.thr = a.thr + y0 * fBQ;
+    b.count = a.count + y0 * fBQ * kCountStride;
+    b.cand = a.cand + y0 * fBQ * (int64_t)a.cap;
+    if (a.cand_ub) b.cand_ub = a.cand_ub + y0 * fBQ * (int64_t)a.cap;
+    b.nq = a.nq - y0 * fBQ;
+    void* args[] = {(void*)&b};
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(fThreads), args,
+                                   smem, stream);
+    if (e != hipSuccess) {
+      set_error("filter_img3_kernel launch: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+  }
+  return check_launch("filter_img3_kernel");
+}
+#endif  // FX_FILTER_IMG3
+
+#if FX_FILTER_IMG3
+// [lb, ub] of a (row, query) pair from the fp16 product x, the row value rv
+// (cosine max(|x|, 1e-12), IP |x|, L2 |x|^2; NaN: forced) and the query's
+// {c1, c0, A, B} (filter_query_table)
+template <int METRIC>
+__device__ __forceinline__ void i4_bounds(float x, float rv, const f32x4& qc, float& lb,
+                                          float& ub) {
+  const float qc1 = qc[0], qc0 = qc[1], qA = qc[2], qB = qc[3];
+  if constexpr (METRIC == 0) {
+    const float s2 = rv + qc0;
+    const float d2 = fmaf(x, qc1, s2);
+    const float e = fmaf(qA, s2, qB);
+    lb = sqrtf(fmaxf(d2 - e, 0.f));
+    ub = sqrtf(d2 + e);
+  } else if constexpr (METRIC == 1) {
+    const float e = fmaf(qA, rv, qB);
+    lb = fmaf(x, qc1, -e);
+    ub = fmaf(x, qc1, e);
+  } else {
+    const float rt = 1.f / rv;
+    const float dist = fmaf(x * rt, qc1, 0.5f);
+    const float e = fmaf(qB, rt, qA);
+    lb = dist - e;
+    ub = dist + e;
+  }
+  if (!(qA <= 3.4e38f) || rv != rv) {  // forced: below / above every key
+    lb = -__builtin_inff();
+    ub = __builtin_nanf("");
+  }
+}
+
+#endif
+
+// ------------------------------ tiled image, both operands by LDS-DMA rings
+#if !FX_FILTER_IMG3  // (the 256-query, 32-wide-K build only)
+#undef FX_FILTER_IMG5
+#define FX_FILTER_IMG5 0
+#endif
+#ifndef FX_FILTER_IMG5
+#define FX_FILTER_IMG5 0
+#endif
+#if FX_FILTER_IMG5
+//
+// filter_img5_kernel: filter_img3_kernel with the image by LDS-DMA too and
+// the appends straight to the candidate buffer:
+//   * each wave DMAs its own 32-row tile's K chunk (2 KB) into a ring of
+//     FX_I5_XA + 1 slots, FX_I5_XA chunks ahead, and reads its A fragments
+//     back from where the DMA put them (lane L's 16 B at +16 L: no conflicts);
+//     the image needs no barrier (a wave reads only its own pieces) and no
+//     registers, so it runs deeper than register stages allow;
+//   * a workgroup appends to its own region of each query's candidate
+//     buffer, cap / gridDim.x slots from slot blockIdx.x * that, positions
+//     from an LDS counter: no global atomic with a return value (which
+//     would wait for the whole prefetched stream) and no flush.  A region
+//     that fills marks its query overflowed (count bit 31): the exact
+//     fallback recomputes it.  At the end every count is raised to cap, so
+//     the rescoring walks every slot (empty ones are skipped).
+#ifndef FX_I5_QA
+#define FX_I5_QA 3
+#endif
+#ifndef FX_I5_XA
+#define FX_I5_XA 4
+#endif
+#ifndef FX_I5_SCHED
+#define FX_I5_SCHED 1  // fragment reads grouped ahead of each k-step's MFMAs
+#endif
+constexpr int kI5QSlots = FX_I5_QA + 1, kI5XSlots = FX_I5_XA + 1;
+constexpr int kI5XBytes = fBM * fBK * 2;  // one image slot: every wave's 2 x 1 KB
+static_assert(FX_I5_QA < FX_I5_XA, "img5: an image chunk is issued before its query chunk");
+struct Img5Shared {
+  unsigned char qring[kI5QSlots][kI3QBytes];
+  unsigned char xring[kI5XSlots][kI5XBytes];
+  float rinfo[fBM];
+  float rterm[fBM];
+  uint32_t rflags[2][kRowFlagWords];
+  f32x4 qtab[fBQ];
+  float2 qab[fBQ];
+  uint32_t qcount[fBQ];  // this workgroup's appends per query
+};
+static_assert(sizeof(Img5Shared) <= 160 * 1024, "filter_img5_kernel: LDS over 160 KB");
+
+template <int METRIC>
+__device__ __forceinline__ void i5_epilogue(const f32x16 (&acc)[kI2QT], const float* rinfo,
+                                            const float* rterm, const uint32_t* flags,
+                                            const f32x4* qtab, const float2* qab,
+                                            const FilterArgs& a, int64_t q0, int64_t r0, int wid,
+                                            int h, int l32, uint32_t* qcount, uint32_t region,
+                                            int diag) {
+  const int lr0 = wid * 32 + 4 * h;
+  f32x4 rv4[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) rv4[g] = *reinterpret_cast<const f32x4*>(rinfo + lr0 + 8 * g);
+  const uint32_t fmask = flags[wid * 2 + h], smask = flags[16 + wid * 2 + h];
+  uint32_t pm[kI2QT];
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u) {
+    const float2 ab = qab[u * 32 + l32];
+    const f32x2 na = {-ab.x, -ab.x}, nb = {-ab.y, -ab.y};
+    uint32_t fail = 0u;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      const f32x4 r = rv4[i >> 1];
+      const f32x2 rp = (i & 1) ? f32x2{r[2], r[3]} : f32x2{r[0], r[1]};
+      const f32x2 xp = {acc[u][2 * i], acc[u][2 * i + 1]};
+      const f32x2 dd = __builtin_elementwise_fma(na, rp, xp) + nb;
+      fail = __builtin_amdgcn_alignbit(fail, __float_as_uint(dd[1]), 31);
+      fail = __builtin_amdgcn_alignbit(fail, __float_as_uint(dd[0]), 31);
+    }
+    pm[u] = (diag & 1) ? 0u : (~fail | fmask) & ~smask & 0xffffu;
+    if (q0 + u * 32 + l32 >= a.nq) pm[u] = 0u;
+  }
+  uint32_t any = 0u;
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u) any |= pm[u];
+  if (__ballot(any != 0u) == 0ull) return;
+  uint32_t pos[kI2QT];
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u)
+    pos[u] = pm[u] != 0u ? atomicAdd(&qcount[u * 32 + l32], (uint32_t)__popc(pm[u])) : 0u;
+  static_for<kI2QT>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    if (__ballot(pm[u] != 0u) == 0ull) return;
+    const int qi = u * 32 + l32;
+    // (opaque: per-query addresses hoisted out of the tile loop were spilled)
+    const int64_t gq = q0 + (int)opaque((unsigned)qi);
+    uint32_t bits = pm[u], p = pos[u];
+    if (bits != 0u && p + (uint32_t)__popc(bits) > region)  // the region is full: overflowed
+      atomicOr(&a.count[gq * kCountStride], 0x80000000u);
+    const f32x4 qc = qtab[qi];
+    uint64_t* cl = a.cand + (size_t)gq * a.cap + (size_t)blockIdx.x * region;
+    uint64_t* cu = a.cand_ub != nullptr ? a.cand_ub + (size_t)gq * a.cap + (size_t)blockIdx.x * region
+                                        : nullptr;
+    while (bits != 0u && p < region) {
+      const int j = __builtin_ctz(bits);
+      bits &= bits - 1u;
+      auto pick = [](float lo, float hi, uint32_t m) {
+        return __uint_as_float((__float_as_uint(hi) & m) | (__float_as_uint(lo) & ~m));
+      };
+      const uint32_t m0 = 0u - ((uint32_t)j & 1u), m1 = 0u - (((uint32_t)j >> 1) & 1u);
+      const uint32_t m2 = 0u - (((uint32_t)j >> 2) & 1u), m3 = 0u - (((uint32_t)j >> 3) & 1u);
+      float v8[8], v4[4], v2[2];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v8[i] = pick(acc[u][2 * i], acc[u][2 * i + 1], m0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v4[i] = pick(v8[2 * i], v8[2 * i + 1], m1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) v2[i] = pick(v4[2 * i], v4[2 * i + 1], m2);
+      const float x = pick(v2[0], v2[1], m3);
+      const int lr = lr0 + (j & 3) + 8 * (j >> 2);
+      const float rv = rinfo[lr];
+      float lb, ub;
+      if constexpr (METRIC == 2) {  // (i4_bounds recomputes 1 / rv; the row's is in LDS)
+        const float rt = rterm[lr];
+        const float dist = fmaf(x * rt, qc[0], 0.5f);
+        const float e = fmaf(qc[3], rt, qc[2]);
+        lb = dist - e;
+        ub = dist + e;
+        if (!(qc[2] <= 3.4e38f) || rv != rv) {
+          lb = -__builtin_inff();
+          ub = __builtin_nanf("");
+        }
+      } else {
+        i4_bounds<METRIC>(x, rv, qc, lb, ub);
+      }
+      const uint32_t grow = (uint32_t)(a.row_base + r0) + (uint32_t)lr;
+      if (cu != nullptr) {
+        cl[p] = make_comp(lb, grow);
+        cu[p] = make_comp(ub, grow);
+      } else {
+        cl[p] = make_comp(ub, grow);
+      }
+      ++p;
+    }
+  });
+}
+
+template <int N>
+__device__ __forceinline__ void i5_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int METRIC>
+__global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img5_kernel(FilterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Img5Shared* sh = reinterpret_cast<Img5Shared*>(smem);
+#ifdef FX_DIAG_BUILD  // FX_FILTER_DIAG as filter_img3_kernel
+  const int diag = a.diag;
+#else
+  constexpr int diag = 0;
+#endif
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, l32 = lane & 31;
+  const int64_t q0 = (int64_t)blockIdx.y * fBQ;
+  const int nch = (a.d + fBK - 1) / fBK;
+  const int ksteps = (a.d + 15) / 16;
+  const int64_t ntile32 = (a.n + 31) / 32;
+  const uint32_t region = (uint32_t)a.cap / gridDim.x;
+  if ((int64_t)blockIdx.x >= a.num_tiles) return;
+  filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
+  for (int q = tid; q < fBQ; q += fThreads) sh->qcount[q] = 0u;
+
+  const __amdgpu_buffer_rsrc_t qr = [&] {
+    const uint64_t qp = reinterpret_cast<uint64_t>(a.Qh + q0 * 32);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)qp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(qp >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane(
+        (int)(((int64_t)(a.dq / 32 - 1) * a.qstride + fBQ) * 64));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             nb, 0x00020000);
+  }();
+  uint32_t qv[kI3QDma];
+#pragma unroll
+  for (int i = 0; i < kI3QDma; ++i) {
+    const int j = wid * kI3QDma + i;
+    const int q = 16 * j + (lane >> 2);
+    qv[i] = (uint32_t)(q * 64 + (((lane & 3) ^ ((q >> 2) & 3)) * 16));
+  }
+  auto issue_q = [&](int c, int slot) {
+    if (diag & 8) return;
+    unsigned char* st = sh->qring[slot];
+#pragma unroll
+    for (int i = 0; i < kI3QDma; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (i3_lds_ptr)(st + (wid * kI3QDma + i) * 1024), 16,
+                                               qv[i], (int)(c * a.qstride * 64), 0, 0);
+  };
+  auto x_rsrc = [&](int64_t ti) {
+    const int64_t t32 = (a.tile_start + ti * a.tile_stride) * (fBM / 32) + wid;
+    const int64_t live = (ti < a.num_tiles && t32 < ntile32) ? 1 : 0;
+    const unsigned char* base = reinterpret_cast<const unsigned char*>(a.X) +
+                                (live ? t32 : 0) * (int64_t)ksteps * 1024;
+    const uint64_t xp = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xp >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)(live * ksteps * 1024));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             nb, 0x00020000);
+  };
+  const uint32_t xl = (uint32_t)opaque(lane) * 16u;
+  // this wave's K chunk c of its 32-row tile into image slot `slot`: k-step
+  // s lands at +(2 w + s) KB, lane L's 16 B at +16 L (its A fragment)
+  auto issue_x = [&](__amdgpu_buffer_rsrc_t xr, int c, int slot) {
+    unsigned char* st = sh->xring[slot] + wid * 2048;
+#pragma unroll
+    for (int s = 0; s < kI2KS; ++s) {
+      const int ks = c * kI2KS + s;
+      const uint32_t off = (ks < ksteps && !(diag & 32)) ? xl : 0x7fff0000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (i3_lds_ptr)(st + s * 1024), 16, off, ks * 1024,
+                                               0, 2 /* nt */);
+    }
+  };
+  uint32_t bq[kI2KS];
+#pragma unroll
+  for (int s = 0; s < kI2KS; ++s) {
+    const int Q = (int)opaque((unsigned)l32);
+    bq[s] = (uint32_t)(Q * 64 + (((2 * s + h) ^ ((Q >> 2) & 3)) * 16));
+  }
+  const uint32_t xrd = (uint32_t)wid * 2048u + xl;  // this lane's A fragment in an image slot
+  f32x16 acc[kI2QT];
+  auto compute = [&](int qs, int xs) {
+    if (diag & 4) return;
+    const unsigned char* st = sh->qring[qs];
+    const unsigned char* sx = sh->xring[xs];
+#pragma unroll
+    for (int s = 0; s < kI2KS; ++s) {
+      const f16x8 av = *reinterpret_cast<const f16x8*>(sx + xrd + s * 1024);
+      f16x8 bv[kI2QT];
+#pragma unroll
+      for (int u = 0; u < kI2QT; ++u)
+        bv[u] = *reinterpret_cast<const f16x8*>(st + bq[s] + u * 32 * 64);
+#pragma unroll
+      for (int u = 0; u < kI2QT; ++u)
+        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv[u], acc[u], 0, 0, 0);
+#if FX_I5_SCHED
+      // the k-step's 9 fragment reads first, then its 8 MFMAs: the reads'
+      // latency is paid once per k-step, not before every MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 9, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+#endif
+    }
+  };
+
+  // ---- prologue: query chunks 0 .. QA-1 and image chunks 0 .. XA-1
+  int qc = 0, qslot = 0;
+#pragma unroll
+  for (int i = 0; i < FX_I5_QA; ++i) {
+    issue_q(qc, qslot);
+    qc = qc + 1 == nch ? 0 : qc + 1;
+    qslot = qslot + 1 == kI5QSlots ? 0 : qslot + 1;
+  }
+  int64_t xt = blockIdx.x;
+  int xc = 0, xslot = 0;
+  __amdgpu_buffer_rsrc_t xr = x_rsrc(xt);
+#pragma unroll
+  for (int i = 0; i < FX_I5_XA; ++i) {
+    issue_x(xr, xc, xslot);
+    xslot = xslot + 1 == kI5XSlots ? 0 : xslot + 1;
+    if (++xc == nch) {
+      xc = 0;
+      xt += gridDim.x;
+      xr = x_rsrc(xt);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (once: the prologue's order differs)
+  int rq = 0, rx = 0;  // slots the next step reads
+  int par = 0;
+  for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
+    const int64_t r0 = (a.tile_start + ti * a.tile_stride) * fBM;
+    if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;
+#pragma unroll
+    for (int u = 0; u < kI2QT; ++u) acc[u] = f32x16(0.f);
+    float rsum = 0.f;
+    uint32_t mword = 0u;
+    for (int c = 0; c < nch; ++c) {
+      // query chunk c landed for every wave (this wave's image chunk c, issued
+      // a step before it, with it), and every wave done with the slots refilled
+      if (diag & 16)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else
+        i5_wait_barrier<kI2KS + (FX_I5_QA - 1) * (kI3QDma + kI2KS)>();
+      issue_q(qc, qslot);
+      qc = qc + 1 == nch ? 0 : qc + 1;
+      qslot = qslot + 1 == kI5QSlots ? 0 : qslot + 1;
+      issue_x(xr, xc, xslot);
+      xslot = xslot + 1 == kI5XSlots ? 0 : xslot + 1;
+      if (++xc == nch) {
+        xc = 0;
+        xt += gridDim.x;
+        xr = x_rsrc(xt);
+      }
+      if (c == 0) {  // the rows' image sums and mask words of this tile
+        const int lr = tid & (fBM - 1);
+        const int64_t row = r0 + lr < a.n ? r0 + lr : a.n - 1;
+        rsum = a.rowinfo[row];
+        const bool masked = a.mask != nullptr;
+        const uint32_t* mp = masked ? a.mask + (row >> 5)
+                                    : reinterpret_cast<const uint32_t*>(a.rowinfo) + row;
+        mword = *mp | (masked ? 0u : ~0u);
+      }
+      compute(rq, rx);
+      rq = rq + 1 == kI5QSlots ? 0 : rq + 1;
+      rx = rx + 1 == kI5XSlots ? 0 : rx + 1;
+    }
+    if (tid < fBM) {  // one thread per row: bound factor, flags
+      const int lr = (int)opaque((unsigned)tid);
+      const int64_t row = r0 + lr;
+      bool ok = row < a.n && ((mword >> (row & 31)) & 1u);
+      const float s = ok ? rsum : 0.f;
+      float rv;
+      if constexpr (METRIC == 0) {
+        rv = s;
+      } else if constexpr (METRIC == 1) {
+        rv = sqrtf(s);
+      } else {
+        rv = fmaxf(sqrtf(s), 1e-12f);
+      }
+      if (!(s <= 3.4e38f)) rv = __builtin_nanf("");
+      filter_note_row<METRIC, 1>(sh->rinfo, sh->rterm, sh->rflags[par], lr, rv, ok);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (diag & 2) {
+      if (acc[0][0] == 1.2345f) a.count[0] = 7;
+    } else {
+      i5_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rflags[par], sh->qtab, sh->qab, a, q0,
+                          r0, wid, h, l32, sh->qcount, region, diag);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // every count at least cap: the rescoring walks every slot of the regions
+  for (int q = tid; q < fBQ; q += fThreads)
+    if (q0 + q < a.nq) atomicMax(&a.count[(q0 + q) * kCountStride], (uint32_t)a.cap);
+}
+
+static int launch_img5(const FilterArgs& a, int metric, hipStream_t stream) {
+  const size_t smem = sizeof(Img5Shared);
+  const void* fn = metric == FX_METRIC_COS ? (const void*)filter_img5_kernel<2>
+                   : metric == FX_METRIC_IP ? (const void*)filter_img5_kernel<1>
+                                            : (const void*)filter_img5_kernel<0>;
   if (int rc = allow_lds(fn)) return rc;
   int cus = 0;
   int rc = device_cus(&cus);
@@ -1554,13 +2232,13 @@ static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
     hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(fThreads), args,
                                    smem, stream);
     if (e != hipSuccess) {
-      set_error("filter_img3_kernel launch: %s", hipGetErrorString(e));
+      set_error("filter_img5_kernel launch: %s", hipGetErrorString(e));
       return FX_EHIP;
     }
   }
-  return check_launch("filter_img3_kernel");
+  return check_launch("filter_img5_kernel");
 }
-#endif  // FX_FILTER_IMG3
+#endif  // FX_FILTER_IMG5
 
 // ------------------------- tiled image, one wave per SIMD, 64-row wave tiles
 #if !FX_FILTER_IMG3  // (the 256-query, 32-wide-K build only)
@@ -1602,36 +2280,6 @@ static_assert(sizeof(Img4Shared) <= 160 * 1024, "filter_img4_kernel: LDS over 16
 constexpr int kI4QDma = kI3QBytes / 1024 / kI4Waves;  // 1-KB query DMAs per wave per chunk
 constexpr int kI4XLd = 2 * kI2KS;                     // image loads per wave per chunk
 static_assert(kI4QDma * 1024 * kI4Waves == kI3QBytes && kI4Waves * 64 == fBM, "img4 tiling");
-
-// [lb, ub] of a (row, query) pair from the fp16 product x, the row value rv
-// (cosine max(|x|, 1e-12), IP |x|, L2 |x|^2; NaN: forced) and the query's
-// {c1, c0, A, B} (filter_query_table)
-template <int METRIC>
-__device__ __forceinline__ void i4_bounds(float x, float rv, const f32x4& qc, float& lb,
-                                          float& ub) {
-  const float qc1 = qc[0], qc0 = qc[1], qA = qc[2], qB = qc[3];
-  if constexpr (METRIC == 0) {
-    const float s2 = rv + qc0;
-    const float d2 = fmaf(x, qc1, s2);
-    const float e = fmaf(qA, s2, qB);
-    lb = sqrtf(fmaxf(d2 - e, 0.f));
-    ub = sqrtf(d2 + e);
-  } else if constexpr (METRIC == 1) {
-    const float e = fmaf(qA, rv, qB);
-    lb = fmaf(x, qc1, -e);
-    ub = fmaf(x, qc1, e);
-  } else {
-    const float rt = 1.f / rv;
-    const float dist = fmaf(x * rt, qc1, 0.5f);
-    const float e = fmaf(qB, rt, qA);
-    lb = dist - e;
-    ub = dist + e;
-  }
-  if (!(qA <= 3.4e38f) || rv != rv) {  // forced: below / above every key
-    lb = -__builtin_inff();
-    ub = __builtin_nanf("");
-  }
-}
 
 // One accumulator element, read from its AGPR by v_accvgpr_read: a plain
 // VALU use makes the allocator copy whole accumulator tuples into VGPRs
@@ -2348,7 +2996,9 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
   if (a.num_tiles <= 0) return FX_OK;
   const bool f16 = a.dtype == FX_DTYPE_F16;
   if (a.rowinfo != nullptr && image_tiled()) {  // the image in MFMA fragment order
-#if FX_FILTER_IMG4
+#if FX_FILTER_IMG5
+    return launch_img5(a, metric, stream);
+#elif FX_FILTER_IMG4
     return launch_img4(a, metric, stream);
 #elif FX_FILTER_IMG3
     return launch_img3(a, metric, stream);
@@ -2455,6 +3105,8 @@ bool filter_ring() { return diag_env("FX_FILTER_RING", 0) != 0; }
 // Batches of <= 64 queries take the 64-query tiles, 65..128 the 128-query ones
 // (their Qh is padded to 64 / 128, filter_query_pad)
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
+  // int8 images: the 256-query kernel for every batch (its queries padded to 256)
+  if (a.img8) return q256::launch(a, metric, stream);
   if (a.nq <= 64) return q64::launch(a, metric, stream);
   if (a.nq <= 128 && !filter_ring()) return q128::launch(a, metric, stream);
   // tiled images: K chunks of 32 (5.07-5.10 vs 5.48-5.49 ms for configs[2]
@@ -2661,6 +3313,201 @@ int launch_image(const float* X, int64_t n, int d, void* img, float* rowinfo,
 #else
   return FX_EUNSUPPORTED;  // (unreachable: image_tiled() is constant)
 #endif
+}
+
+// ---- int8 filter image (filter_img3_kernel<METRIC, true>; the bounds are
+// derived above filter_img3_kernel).  Rows and queries are scaled so that
+// their integer images have norm <= 2048 (|x~ . q~| <= 2^22):
+//   s = max(max|x| / 127, |x| / (2046 - sqrt(d) / 2)).
+__device__ __forceinline__ float i8_norm_cap(int d) { return 2046.f - 0.5f * sqrtf((float)d); }
+
+typedef float img_f32x16 __attribute__((ext_vector_type(16)));
+
+// The image in MFMA fragment order: [ceil(n / 32) row tiles][ceil(d / 32)
+// k-steps][64 lanes][16 B]: lane l holds components 32 s + 16 (l / 32) .. + 15
+// of row 32 t + l % 32 (the v_mfma_i32_32x32x32_i8 A operand), and per row
+// {omega = w + kappa v, 1/s, N/s, n^2/s} (NaN omega: forced).  One wave per
+// 32-row tile: a pass for max |x| and n^2, a pass that quantizes, writes and
+// accumulates the residual (|x - s x~|^2 in f32 with (d + 8) u slack) and
+// w^2 (exact in integers).  d % 8 == 0 (fx_filter_image8 checks).
+__global__ void __launch_bounds__(256) image8_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                    int8_t* __restrict__ img,
+                                                    float* __restrict__ rowinfo) {
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int64_t nt = (n + 31) / 32;
+  const int ksteps = (d + 31) / 32;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const float u = 5.9604644775390625e-08f;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < nt; t += nw) {
+    const int64_t r = t * 32 + (lane & 31);
+    const bool live = r < n;
+    const float* xr = X + (live ? r : 0) * (int64_t)d;
+    auto load = [&](int ks) {  // components 32 ks + 16 h .. + 15 (zeros past d)
+      img_f32x16 v;
+      const int k0 = 32 * ks + 16 * h;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + 4 * j;
+        const img_f32x4 q4 = (live && k < d) ? *reinterpret_cast<const img_f32x4*>(xr + k)
+                                              : img_f32x4(0.f);
+        v[4 * j] = q4[0];
+        v[4 * j + 1] = q4[1];
+        v[4 * j + 2] = q4[2];
+        v[4 * j + 3] = q4[3];
+      }
+      return v;
+    };
+    float m = 0.f, n2 = 0.f;
+    for (int ks = 0; ks < ksteps; ++ks) {
+      const img_f32x16 v = load(ks);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        n2 = fmaf(v[e], v[e], n2);
+        m = fmaxf(m, fabsf(v[e]));
+      }
+    }
+    n2 += __shfl_xor(n2, 32);
+    m = fmaxf(m, __shfl_xor(m, 32));
+    const bool finite = m <= 3.4e38f && n2 <= 3.4e38f;
+    const float nrm = sqrtf(n2);
+    float sc = fmaxf(m * (1.f / 127.f), nrm / i8_norm_cap(d));
+    if (!(sc > 1e-30f) || !finite) sc = 1.f;  // zero / tiny / non-finite rows (forced below)
+    const float is = 1.f / sc;
+    int w2 = 0;
+    float e2 = 0.f;
+    int8_t* out = img + (t * ksteps) * 1024 + lane * 16;
+    for (int ks = 0; ks < ksteps; ++ks) {
+      const img_f32x16 v = load(ks);
+      int32_t packed[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t word = 0u;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const float x = v[4 * j + b];
+          float qf = rintf(x * is);
+          qf = fminf(fmaxf(qf, -127.f), 127.f);
+          if (!finite) qf = 0.f;
+          const int qi = (int)qf;
+          w2 += qi * qi;
+          const float res = fmaf(-sc, qf, x);
+          e2 = fmaf(res, res, e2);
+          word |= ((uint32_t)qi & 0xffu) << (8 * b);
+        }
+        packed[j] = (int32_t)word;
+      }
+      *reinterpret_cast<int4*>(out + ks * 1024) = make_int4(packed[0], packed[1], packed[2], packed[3]);
+    }
+    w2 += __shfl_xor(w2, 32);
+    e2 += __shfl_xor(e2, 32);
+    if (h == 0 && live) {
+      const float e = sqrtf(e2 * (1.f + 2.f * (float)(d + 8) * u)) * (1.f + 4.f * u);
+      const float w = sqrtf((float)w2) * (1.f + 2.f * u);
+      const float v = e * is * (1.f + 4.f * u);
+      float om = (w + kI8Kappa * v) * (1.f + 4.f * u);
+      const bool tiny = !(m == 0.f) && !(fmaxf(m * (1.f / 127.f), nrm / i8_norm_cap(d)) > 1e-30f);
+      if (!finite || tiny || w > 2048.f || !(om <= 3.4e38f)) om = __builtin_nanf("");
+      const float nn = fmaxf(nrm, 1e-12f);
+      img_f32x4 info = {om, is, nn * is, n2 * is};
+      *reinterpret_cast<img_f32x4*>(rowinfo + r * kI8RowInfo) = info;
+    }
+  }
+}
+
+int launch_image8(const float* X, int64_t n, int d, void* img, float* rowinfo,
+                  hipStream_t stream) {
+  if (n <= 0) return FX_OK;
+  int cus = 0;
+  int rc = device_cus(&cus);
+  if (rc) return rc;
+  int64_t blocks = ((n + 31) / 32 + 3) / 4;
+  if (blocks > (int64_t)cus * 8) blocks = (int64_t)cus * 8;
+  hipLaunchKernelGGL(image8_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, n, d,
+                     reinterpret_cast<int8_t*>(img), rowinfo);
+  return check_launch("image8_kernel");
+}
+
+// Per query (one wave): q~ = rint(q / s_q) in int8, zero-padded to dq, in
+// 64-component chunks, query-major inside a chunk (chunk c of query q: 64 B
+// at (c * nq_pad + q) * 64), and {s_q, R', n_q^2, |q|} with
+// R' = max(R, P / kappa) (see "int8 filter image"); sums in double (products
+// of f32 and of f32 x int8 are exact there).  A non-finite query, or one whose
+// integer image exceeds norm 2048: R' = +inf (forced).
+__global__ void qprep8_kernel(const float* __restrict__ Q, int64_t nq, int64_t nq_pad, int d,
+                              int dq, int metric, int8_t* __restrict__ Qb,
+                              float* __restrict__ qinfo) {
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (q >= nq_pad) return;
+  auto at = [&](int i) -> int8_t& {
+    return Qb[((int64_t)(i >> 6) * nq_pad + q) * 64 + (i & 63)];
+  };
+  if (q >= nq) {
+    for (int i = lane; i < dq; i += 64) at(i) = 0;
+    return;
+  }
+  const float* qv = Q + q * (int64_t)d;
+  double s2 = 0.0;
+  float m = 0.f;
+  for (int i = lane; i < d; i += 64) {
+    s2 = fma((double)qv[i], (double)qv[i], s2);
+    m = fmaxf(m, fabsf(qv[i]));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    s2 += __shfl_xor(s2, o);
+    m = fmaxf(m, __shfl_xor(m, o));
+  }
+  const bool finite = m <= 3.4e38f && s2 <= 1e76;
+  const double nq_ = sqrt(s2);
+  float sc = fmaxf(m * (1.f / 127.f), (float)(nq_ / (double)i8_norm_cap(d)) * (1.f + 1e-6f));
+  const bool tiny = m != 0.f && !(sc > 1e-30f);
+  if (!(sc > 1e-30f) || !finite) sc = 1.f;
+  const float is = 1.f / sc;
+  double e2 = 0.0;
+  int w2 = 0;
+  for (int i = lane; i < dq; i += 64) {
+    int qi = 0;
+    if (i < d && finite) {
+      float qf = rintf(qv[i] * is);
+      qf = fminf(fmaxf(qf, -127.f), 127.f);
+      qi = (int)qf;
+      const double r = (double)qv[i] - (double)sc * (double)qi;  // exact
+      e2 = fma(r, r, e2);
+    }
+    w2 += qi * qi;
+    at(i) = (int8_t)qi;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    e2 += __shfl_xor(e2, o);
+    w2 += __shfl_xor(w2, o);
+  }
+  if (lane == 0) {
+    const double u = 5.9604644775390625e-08;
+    const double g = (double)(d + 2) * u * 1.01;
+    const double eq = sqrt(e2) * (1.0 + 1e-12);
+    double P = nq_ / sc, R = eq / sc;
+    if (metric == FX_METRIC_IP) {
+      R += g * nq_ / sc;
+      P *= 1.0 + g;
+    }
+    double rp = R > P / (double)kI8Kappa ? R : P / (double)kI8Kappa;
+    rp *= 1.0 + 1e-6;
+    if (!finite || tiny || sqrt((double)w2) > 2048.0) rp = __builtin_inf();
+    float* info = qinfo + q * kI8QInfo;
+    info[0] = sc;
+    info[1] = __double2float_ru(rp);
+    info[2] = (float)s2;
+    info[3] = (float)nq_;
+  }
+}
+
+int launch_qprep8(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
+                  int8_t* Qb, float* qinfo, hipStream_t stream) {
+  hipLaunchKernelGGL(qprep8_kernel, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, stream, Q,
+                     nq, nq_pad, d, dq, metric, Qb, qinfo);
+  return check_launch("qprep8_kernel");
 }
 
 #endif  // FX_FILTER_VARIANT

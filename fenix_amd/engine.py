@@ -424,15 +424,16 @@ class Engine:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def filter_image(self, shard: Shard, nq: int, k: int,
-                     metric: int) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
-        """The fp16 filter image (+ row sums of squares) of an f32 shard for a
-        search that runs the batched filter (fx_filter_image_used), built on
-        first use and kept while the corpus tensor lives and is unmodified;
-        (None, None) when the search does not read one, when
-        ``FENIX_AMD_FILTER_IMAGE=0``, or when the HBM budget (``Residency``)
-        cannot hold it.  The filter only selects candidates, which are
-        rescored from the f32 rows, so results never depend on whether an
-        image is used.
+                     metric: int) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], int]:
+        """The filter image of an f32 shard for a search that runs the batched
+        filter (fx_filter_image_used): (image, rowinfo, bits), bits 8
+        (fx_filter_image8, the default) or 16 (fx_filter_image) as the library
+        option "filter_image" says, built on first use and kept while the
+        corpus tensor lives and is unmodified; (None, None, 0) when the search
+        does not read one, when the option is 0 (or ``FENIX_AMD_FILTER_IMAGE=0``),
+        or when the HBM budget (``Residency``) cannot hold it.  The filter only
+        selects candidates, which are rescored from the f32 rows, so results
+        never depend on whether or which image is used.
 
         Invariant: an image is valid only while its corpus is unchanged.
         Staleness is detected through the tensor's identity, data pointer,
@@ -443,48 +444,52 @@ class Engine:
 
         The image is built on the caller's current stream; a search on another
         stream waits for the build through an event recorded after it."""
-        if (shard.dtype_id != _lib.DTYPE_F32
+        none = (None, None, 0)
+        bits = _lib.get_option("filter_image")
+        if (shard.dtype_id != _lib.DTYPE_F32 or bits not in (8, 16)
                 or os.environ.get("FENIX_AMD_FILTER_IMAGE", "1") == "0"
                 or not _lib.filter_image_used(shard.n, shard.d, shard.dtype_id, nq, k, metric)):
-            return None, None
+            return none
         t = shard.data
         # an unaligned corpus takes the scan's scalar-load variant, never the
         # batched filter (fx_filter_image_used assumes 16-B aligned rows)
         if not t.is_contiguous() or t.data_ptr() % 16 != 0:
-            return None, None
+            return none
         key = id(t)
         rkey = ("image", self.device.index, key)
-        sig = (t.data_ptr(), tuple(t.shape), t._version)
+        sig = (t.data_ptr(), tuple(t.shape), t._version, bits)
         hit = self._images.get(key)
         if hit is not None and hit[0] == sig:
             RESIDENT.touch(rkey)
             torch.cuda.current_stream(self.device).wait_event(hit[3])
-            return hit[1], hit[2]
+            return hit[1], hit[2], bits
         self.invalidate_image(t)  # a stale image: free it before building the new one
         n, d = shard.n, shard.d
+        L = _lib.load()
+        sizes, build = ((L.fx_filter_image8_bytes, L.fx_filter_image8) if bits == 8
+                        else (L.fx_filter_image_bytes, L.fx_filter_image))
         ib, rb = ctypes.c_size_t(0), ctypes.c_size_t(0)
-        _lib.check(_lib.load().fx_filter_image_bytes(n, d, ctypes.byref(ib), ctypes.byref(rb)))
+        _lib.check(sizes(n, d, ctypes.byref(ib), ctypes.byref(rb)))
         need = ib.value + rb.value
         if not RESIDENT.reserve({self.device.index: need}):
-            return None, None
+            return none
         free, _ = torch.cuda.mem_get_info(self.device)
         cached = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
         if need + (1 << 30) > free + cached:
-            return None, None
+            return none
         try:
-            img = torch.empty((ib.value // 2,), dtype=torch.float16, device=self.device)
-            info = torch.empty((n,), dtype=torch.float32, device=self.device)
+            img = torch.empty((ib.value,), dtype=torch.uint8, device=self.device)
+            info = torch.empty((rb.value // 4,), dtype=torch.float32, device=self.device)
         except torch.cuda.OutOfMemoryError:
-            return None, None  # the f32 filter (no image) is always correct
-        _lib.check(_lib.load().fx_filter_image(_ptr(t), n, d, _ptr(img), _ptr(info),
-                                               self._stream()))
+            return none  # the f32 filter (no image) is always correct
+        _lib.check(build(_ptr(t), n, d, _ptr(img), _ptr(info), self._stream()))
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self._images[key] = (sig, img, info, ev)
         RESIDENT.add(rkey, Residency.IMAGE, {self.device.index: need},
                      lambda: self._images.pop(key, None))
         weakref.finalize(t, self._drop_image, key)
-        return img, info
+        return img, info, bits
 
     def clear_images(self) -> None:
         """Drop every filter image this engine holds."""
@@ -510,9 +515,10 @@ class Engine:
             return
         nbytes = _lib.knn_workspace_bytes(shard.n, shard.d, shard.dtype_id, nq, k)
         ws = self._workspace(nbytes)
-        img, info = self.filter_image(shard, nq, k, metric)
+        img, info, bits = self.filter_image(shard, nq, k, metric)
+        L = _lib.load()
         _lib.check(
-            _lib.load().fx_knn_search_img(
+            (L.fx_knn_search_img8 if bits == 8 else L.fx_knn_search_img)(
                 _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base,
                 _ptr(img), _ptr(info), _ptr(queries), nq, metric, k, _ptr(mask), _ptr(ws),
                 ws.numel(), _ptr(out_dist), _ptr(out_row), self._stream(),
@@ -536,9 +542,10 @@ class Engine:
         nq = queries.shape[0]
         nbytes = _lib.knn_workspace_bytes(shard.n, shard.d, shard.dtype_id, nq, k)
         ws = self._workspace(nbytes)
-        img, info = self.filter_image(shard, nq, k, metric)
+        img, info, bits = self.filter_image(shard, nq, k, metric)
+        L = _lib.load()
         _lib.check(
-            _lib.load().fx_knn_scan_img(
+            (L.fx_knn_scan_img8 if bits == 8 else L.fx_knn_scan_img)(
                 _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base,
                 _ptr(img), _ptr(info), _ptr(queries), nq, metric, k, _ptr(mask), _ptr(ws),
                 ws.numel(), self._stream(),

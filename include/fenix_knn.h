@@ -74,6 +74,10 @@ int fx_device_count(int* out);
  *   "batched"             1  0: each query of a batch runs the single-query scan
  *   "batch_min_queries"   2  smallest batch that takes the batched filter (1:
  *                            single float32 queries too, with a filter image)
+ *   "filter_image"        8  which filter image a host builds for float32
+ *                            corpora: 8 (fx_filter_image8), 16
+ *                            (fx_filter_image) or 0 (none); read by the host
+ *                            (fenix_amd.engine), not by the library's calls
  * Test switches (they change which code runs, never the results):
  *   "batch_cap"           0  candidate buffer per query of the batched filter
  *                            (0: max(64 k, 16 K); smaller than 16 k is ignored)
@@ -184,6 +188,30 @@ int fx_knn_search_img(const void* corpus, int dtype, int64_t n, int64_t d, int64
                       const void* image, const float* rowinfo, const float* queries, int64_t nq,
                       int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
                       float* out_dist, int64_t* out_row, void* stream);
+
+/*
+ * int8 filter image of a float32 corpus: the same role as the fp16 image at a
+ * quarter of the corpus bytes, searched on the int8 matrix cores (twice the
+ * fp16 rate).  fx_filter_image8 writes image (row tiles of 32 rows in MFMA
+ * fragment order, each row scaled to int8 by its own scale) and rowinfo [n][4]
+ * float32 (the row's bound terms; NaN first term = forced through).  The
+ * rigorous bounds are wider than fp16's, so the filter keeps more candidates
+ * and refines its thresholds by exact rescoring; results are the same bits as
+ * fx_knn_scan / fx_knn_search.  d must be a multiple of 8; corpus, image and
+ * rowinfo 16-B aligned; same workspace as fx_knn_scan.  Rebuild whenever the
+ * corpus changes.  Replaces nothing in the reference (see above).
+ */
+int fx_filter_image8_bytes(int64_t n, int64_t d, size_t* image_bytes, size_t* rowinfo_bytes);
+int fx_filter_image8(const float* corpus, int64_t n, int64_t d, void* image, float* rowinfo,
+                     void* stream);
+int fx_knn_scan_img8(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                     const void* image, const float* rowinfo, const float* queries, int64_t nq,
+                     int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
+                     void* stream);
+int fx_knn_search_img8(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                       const void* image, const float* rowinfo, const float* queries, int64_t nq,
+                       int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,
+                       float* out_dist, int64_t* out_row, void* stream);
 
 /*
  * fx_knn_search over a list of corpus rows instead of all of them: rows

@@ -40,7 +40,7 @@ def test_library_is_gfx950():
 
 def test_version_and_limits():
     lib = _lib.load()
-    assert lib.fx_version() == 102  # 1.2: options, device-gated overflow fallback
+    assert lib.fx_version() == 103  # 1.3: int8 filter images (1.2: options, device-gated fallback)
     assert _lib.max_k() == 1024
 
 

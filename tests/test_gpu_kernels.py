@@ -663,14 +663,75 @@ def test_filter_image_contents(eng):
     assert rc != 0
 
 
+def _build_image8(x, n, d):
+    """fx_filter_image8 into buffers of fx_filter_image8_bytes."""
+    import ctypes
+    ib, rb = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    _lib.check(_lib.load().fx_filter_image8_bytes(n, d, ctypes.byref(ib), ctypes.byref(rb)))
+    assert ib.value == (n + 31) // 32 * ((d + 31) // 32) * 1024 and rb.value == n * 16
+    img = torch.empty((ib.value,), dtype=torch.uint8, device=x.device)
+    info = torch.empty((n, 4), dtype=torch.float32, device=x.device)
+    _lib.check(_lib.load().fx_filter_image8(x.data_ptr(), n, d, img.data_ptr(), info.data_ptr(),
+                                            torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    return img, info
+
+
+def test_filter_image8_contents(eng):
+    """fx_filter_image8: rows in the int8 MFMA-fragment layout [tile][k-step]
+    [lane half][row in tile][16]; per row x~ = rint(x / s) with |x~| <= 127,
+    |x~| <= 2048, every component within s/2 of x / s, and the bound terms
+    {omega, 1/s, N/s, n^2/s}: omega >= |x~| + kappa |x - s x~| / s (float64
+    reference), NaN exactly for non-finite rows, 0 for zero rows."""
+    n, d = 5_003, 136
+    xh = _extreme_rows(n, d, 41)
+    x = torch.from_numpy(xh).to(eng.device)
+    img, info = _build_image8(x, n, d)
+    h = img.cpu().numpy().view(np.int8)
+    t, ks = (n + 31) // 32, (d + 31) // 32
+    full = h.reshape(t, ks, 2, 32, 16).transpose(0, 3, 1, 2, 4).reshape(t * 32, ks * 32)
+    assert not full[n:].any() and not full[:, d:].any(), "image padding is not zero"
+    xq = full[:n, :d].astype(np.float64)
+    inf = info.cpu().numpy().astype(np.float64)
+    om, is_, nos, n2s = inf.T
+    with np.errstate(over="ignore", invalid="ignore"):
+        forced = ~np.isfinite(xh).all(axis=1)
+    np.testing.assert_array_equal(np.isnan(om), forced)
+    ok = ~forced
+    zero = ok & ~xh.any(axis=1)
+    assert (om[zero] == 0).all() and not xq[zero].any()
+    live = ok & ~zero
+    s = 1.0 / is_[live]
+    x64 = xh[live].astype(np.float64)
+    res = x64 - s[:, None] * xq[live]
+    assert (np.abs(xq) <= 127).all()
+    w = np.sqrt((xq[live] ** 2).sum(axis=1))
+    assert (w <= 2048).all()
+    assert (np.abs(res) <= 0.5 * s[:, None] * (1 + 1e-5)).all()
+    e = np.sqrt((res ** 2).sum(axis=1))
+    assert (om[live] >= w + 128.0 * e / s).all()
+    assert (om[live] <= (w + 128.0 * e / s) * (1 + 1e-4) + 1e-3).all()
+    nrm = np.sqrt((x64 ** 2).sum(axis=1))
+    np.testing.assert_allclose(nos[live], np.maximum(nrm, 1e-12) / s, rtol=1e-5)
+    np.testing.assert_allclose(n2s[live], nrm ** 2 / s, rtol=1e-5)
+    # argument checks: d not a multiple of 8, misaligned image
+    rc = _lib.load().fx_filter_image8(x.data_ptr(), n, 100, img.data_ptr(), info.data_ptr(), None)
+    assert rc != 0
+    rc = _lib.load().fx_filter_image8(x.data_ptr(), n, d, img.data_ptr() + 2, info.data_ptr(),
+                                      None)
+    assert rc != 0
+
+
+@pytest.mark.parametrize("bits", [8, 16])
 @pytest.mark.parametrize("metric", METRICS)
 @pytest.mark.parametrize("n,d,nq,k", [(100_000, 768, 40, 100), (60_000, 256, 256, 64),
                                       (30_000, 64, 2, 300), (20_000, 136, 70, 25)])
-def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k):
-    """Batched f32 searches through the fp16 filter image (the default) equal
-    the same searches without it (FENIX_AMD_FILTER_IMAGE=0) and the
-    single-query scan, bit for bit, over rows the image cannot represent
-    (beyond fp16 range, infinities, NaN, subnormal, zero)."""
+def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k, bits):
+    """Batched f32 searches through the int8 (the default) and the fp16
+    filter images equal the same searches without one
+    (FENIX_AMD_FILTER_IMAGE=0) and the single-query scan, bit for bit, over
+    rows the images cannot represent (beyond fp16 range, infinities, NaN,
+    subnormal, zero)."""
     xh = _extreme_rows(n, d, 43)
     x = torch.from_numpy(xh).to(eng.device)
     q = O.fill_normal(nq, d, seed=44)
@@ -679,8 +740,9 @@ def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k):
     monkeypatch.delenv("FENIX_AMD_FILTER_IMAGE", raising=False)
     assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, nq, k, _lib.METRICS[metric])
     eng.clear_images()
-    id_, ir = gpu_search(eng, x, q, metric, k)  # MFMA-fragment-order image
-    assert id(x) in eng._images  # the image path ran
+    with _lib.options(filter_image=bits):
+        id_, ir = gpu_search(eng, x, q, metric, k)  # MFMA-fragment-order image
+    assert eng._images[id(x)][0][3] == bits  # the image path ran
     eng.clear_images()
     monkeypatch.setenv("FENIX_AMD_FILTER_IMAGE", "0")
     nd, nr = gpu_search(eng, x, q, metric, k)
@@ -691,16 +753,18 @@ def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k):
         np.testing.assert_array_equal(dd.view(np.uint32), sd.view(np.uint32))
 
 
+@pytest.mark.parametrize("bits", [8, 16])
 @pytest.mark.parametrize("metric", METRICS)
-def test_single_query_through_filter_image(eng, monkeypatch, metric):
+def test_single_query_through_filter_image(eng, monkeypatch, metric, bits):
     """"batch_min_queries" = 1: single queries take the batched filter over
-    the image (64-query tiles, one live query) and still equal the scan bit
-    for bit."""
+    the image (fp16: 64-query tiles, int8: 256-query tiles, one live query)
+    and still equal the scan bit for bit."""
     n, d, k = 80_000, 256, 100
     xh = _extreme_rows(n, d, 45)
     x = torch.from_numpy(xh).to(eng.device)
     monkeypatch.delenv("FENIX_AMD_FILTER_IMAGE", raising=False)
-    with _lib.options(batch_min_queries=1):
+    eng.clear_images()
+    with _lib.options(batch_min_queries=1, filter_image=bits):
         assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, 1, k, _lib.METRICS[metric])
         for seed in (46, 47):
             q = O.fill_normal(1, d, seed=seed)
