@@ -200,7 +200,7 @@ struct BatchLayout {
   int64_t start[16], stride[16], num[16];
   MergePlan merge;
   size_t off_qnorm, off_thr, off_count, off_cand, off_merge, off_cand_ub, off_qh, off_qinfo,
-      off_topd, off_topr, total;
+      off_topd, off_topr, off_kmax, total;
 };
 
 // The fp16-MFMA filter (knn_filter.hip).  Diagnostic builds keep the
@@ -269,6 +269,8 @@ static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, 
     off += align256((size_t)nq * k * 4);
     b->off_topr = off;
     off += align256((size_t)nq * k * 8);
+    b->off_kmax = off;  // launch_exact_kth's per-query maxima and block tickets
+    off += align256((size_t)nq * 16);
   }
   b->total = off;
   return FX_OK;
@@ -336,20 +338,33 @@ static int plan_large_search(int64_t n, int64_t d, int dtype, int64_t nq, int me
 }
 
 // The overflow fallback of the batched path runs the single-query plan over
-// rounds of fq queries; its candidate lists take at most this many bytes
-// (fq = 256 at 10M rows and k = 100, 32 at k = 1 000).
+// rounds of fq queries; its candidate lists take at most this many bytes.
 static constexpr size_t kFallbackListBytes = (size_t)256 << 20;
+
+// Its scan takes at most kFallbackBlocks blocks per query: the gated launch
+// covers every query of a round, and an empty block still occupies its CU's
+// LDS while it starts and exits (256 blocks x 256 queries of 10M x 768: 99 us
+// with nothing to do; 16 per query: a few us, and an overflowing query still
+// streams its rows from 16 CUs).
+static constexpr int64_t kFallbackBlocks = 16;
 
 static int plan_fallback(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
                          bool aligned, SearchLayout* s, int64_t* fq) {
-  int rc = plan_single(n, d, dtype, 1, k, metric, aligned, s);
+  int rc = plan_scan(n, d, dtype, k, metric, aligned, &s->scan);
   if (rc) return rc;
-  int64_t f = (int64_t)(kFallbackListBytes / (s->total > 0 ? s->total : 1));
+  limit_scan_blocks(&s->scan, n, kFallbackBlocks);
+  const size_t per_query = (size_t)s->scan.nlists * k * 8;
+  int64_t f = (int64_t)(kFallbackListBytes / (per_query > 0 ? per_query : 1));
   if (f > nq) f = nq;
   if (f > 65535) f = 65535;
   if (f < 1) f = 1;
   *fq = f;
-  return f == 1 ? FX_OK : plan_single(n, d, dtype, f, k, metric, aligned, s);
+  rc = plan_merge(f, s->scan.nlists, k, k, &s->merge);
+  if (rc) return rc;
+  s->lists_bytes = align256((size_t)f * s->scan.nlists * k * 8);
+  s->total = s->lists_bytes + s->merge.ws_bytes;
+  s->batched = false;
+  return FX_OK;
 }
 
 static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
@@ -425,11 +440,12 @@ static int fallback_search(const SearchLayout& s, const void* corpus, int dtype,
 //
 // An int8 filter image (fx_filter_image8) gives bounds ~30x wider than fp16
 // (per-row 8-bit quantization, see knn_filter.hip "int8 filter image"), so a
-// k-th upper bound would sit well above the k-th distance: after each phase
-// the k candidates with the smallest upper bounds are rescored exactly
-// (launch_exact_kth) and their largest exact composite becomes the
-// threshold (k scan distances lie at or below it), and the samples grow by
-// kI8SampleRatio per phase, which keeps the appends near cap/4 per query.
+// k-th upper bound sits well above the k-th distance: after the last two
+// phases the k candidates with the smallest upper bounds are rescored exactly
+// (launch_exact_kth) and their largest exact composite becomes the threshold
+// (k scan distances lie at or below it), and the samples grow by
+// kI8SampleRatio per phase, which keeps the appends below cap/4 per query
+// (10M x 768 cosine, 256 queries: ~2.5 K, 6 K, 10 K, 4 K per phase).
 static int filter_phases(const BatchLayout& b, const void* X, int dtype, const void* image,
                          const float* rowinfo, bool img8, int64_t n, int64_t d, int64_t row_base,
                          const float* Q, int64_t nq, int metric, int64_t k,
@@ -451,11 +467,11 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
     if (rc) return rc;
   }
   hipError_t e = hipMemsetAsync(thr, 0xFF, (size_t)nq * 8, st);
+  if (img8 && e == hipSuccess) e = hipMemsetAsync(w + b.off_kmax, 0, (size_t)nq * 16, st);
   for (int ph = 0; ph < b.nphases && e == hipSuccess; ++ph) {
     const bool last = ph + 1 == b.nphases;
+    // (the lists are read up to count only: no fill of the candidate buffers)
     e = hipMemsetAsync(count, 0, (size_t)nq * 4 * kCountStride, st);
-    if (e == hipSuccess) e = hipMemsetAsync(cand, 0xFF, (size_t)nq * b.cap * 8, st);
-    if (e == hipSuccess && last) e = hipMemsetAsync(cand_ub, 0xFF, (size_t)nq * b.cap * 8, st);
     if (e != hipSuccess) break;
     FilterArgs a = {};
     a.X = image != nullptr ? image : X;
@@ -468,6 +484,7 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
     a.dq = b.dq;
     a.qstride = img8 ? nq_pad8 : b.nq_pad;
     a.img8 = img8 ? 1 : 0;
+    a.all_pass = ph == 0 ? 1 : 0;  // (thr was just filled with the empty key)
     a.qinfo = qinfo;
     a.nq = nq;
     a.mask = mask;
@@ -482,19 +499,23 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
     a.diag = diag_env("FX_FILTER_DIAG", 0);
     rc = launch_filter(a, metric, st);
     if (rc) return rc;
-    if (img8) {  // the exact distances of the k best upper bounds: next threshold
+    // int8 images, the last two phases: the exact distances of the k best
+    // upper bounds give the next threshold (earlier, small samples: the k-th
+    // upper bound, like fp16; their appends stay far below cap)
+    if (img8 && ph + 2 >= b.nphases) {
       float* topd = reinterpret_cast<float*>(w + b.off_topd);
       int64_t* topr = reinterpret_cast<int64_t*>(w + b.off_topr);
-      rc = run_merge(b.merge, last ? cand_ub : cand, nq, k, w + b.off_merge, topd, topr, st);
+      rc = run_merge(b.merge, last ? cand_ub : cand, nq, k, w + b.off_merge, topd, topr, st,
+                     nullptr, nullptr, 0, count);
       if (rc) return rc;
       rc = launch_exact_kth(X, dtype, n, (int)d, row_base, Q, qnorm, nq, (int)k, topr, metric,
-                            thr, st);
+                            thr, reinterpret_cast<uint64_t*>(w + b.off_kmax), st);
       if (rc) return rc;
       continue;
     }
     // the k-th upper bound of this phase's candidates: next threshold
     rc = run_merge(b.merge, last ? cand_ub : cand, nq, k, w + b.off_merge, nullptr, nullptr, st,
-                   thr);
+                   thr, nullptr, 0, count);
     if (rc) return rc;
   }
   if (e != hipSuccess) {
@@ -882,7 +903,9 @@ int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
   const BatchLayout& b = s.batch;
   char* w = reinterpret_cast<char*>(ws);
   const uint64_t* cand = reinterpret_cast<const uint64_t*>(w + b.off_cand);
-  rc = run_merge(b.merge, cand, nq, k, w + b.off_merge, out_dist, out_row, st);
+  const uint32_t* count = reinterpret_cast<const uint32_t*>(w + b.off_count);
+  rc = run_merge(b.merge, cand, nq, k, w + b.off_merge, out_dist, out_row, st, nullptr, nullptr,
+                 0, count);
   if (rc) return rc;
   // queries whose candidates overflowed `cap`: recomputed exactly, gated on
   // the device ("force_fallback" (test switch): every query)

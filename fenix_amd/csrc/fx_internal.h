@@ -77,6 +77,8 @@ struct ScanPlan {
 };
 
 int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool aligned, ScanPlan* p);
+// at most max_blocks blocks per query (rows_per_block, blocks, nlists recomputed)
+void limit_scan_blocks(ScanPlan* p, int64_t n, int64_t max_blocks);
 int launch_scan(const ScanPlan& p, const ScanArgs& a, int64_t nq, hipStream_t stream);
 
 // Merge of candidate lists: [nq][nlists][kin] composites -> top-k.
@@ -91,10 +93,12 @@ int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p)
 // out_dist/out_row may be null; out_kth (optional) receives each query's k-th
 // smallest composite (kEmpty if fewer than k candidates).
 // gate/gate_cap: as ScanArgs::gate, per query of the merge.
+// count (optional): appended lists, query q's entries are its first
+// count[q * kCountStride] slots (capped at nlists * kin; the rest unread).
 int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, void* ws,
               float* out_dist, int64_t* out_row, hipStream_t stream,
               uint64_t* out_kth = nullptr, const uint32_t* gate = nullptr,
-              int64_t gate_cap = 0);
+              int64_t gate_cap = 0, const uint32_t* count = nullptr);
 
 // Batched queries (knn_batch.hip): fp32 MFMA GEMM + threshold filter.
 struct BatchArgs {
@@ -125,10 +129,11 @@ int launch_rescore(const void* X, int dtype, int64_t n, int d, int64_t row_base,
                    const float* Q, const float* qnorm, int64_t nq, const uint32_t* count,
                    uint64_t* cand, int cap, int metric, const uint64_t* thr, hipStream_t stream);
 // thr[q] = min(thr[q], the largest exact composite of the query's k rows
-// [nq][k] (global, -1 = missing: the query keeps its threshold))
+// [nq][k] (global, -1 = missing: the query keeps its threshold)); scratch
+// [nq][2] uint64 zeroed before the first call (left zeroed by each call)
 int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_base,
                      const float* Q, const float* qnorm, int64_t nq, int k, const int64_t* rows,
-                     int metric, uint64_t* thr, hipStream_t stream);
+                     int metric, uint64_t* thr, uint64_t* scratch, hipStream_t stream);
 
 // Batched filter on the fp16 matrix cores (knn_filter.hip): appends every
 // (row, query) whose rigorous lower bound reaches the query's threshold.
@@ -156,6 +161,8 @@ struct FilterArgs {
                           // img8: [n][kI8RowInfo] (launch_image8)
   int img8;               // X is the int8 filter image (launch_image8), Qh/qinfo from
                           // launch_qprep8
+  int all_pass;           // no query has a threshold yet (thr all empty): img8 appends
+                          // every live pair without the test
   int diag;               // FX_FILTER_DIAG (diagnostic builds only): 1 no appends, 2 no epilogue,
                           // 4 no MFMA, 8 no query loads, 16 no LDS stores,
                           // 32 no append atomics, 64 no append stores

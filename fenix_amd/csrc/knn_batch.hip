@@ -298,25 +298,44 @@ __device__ __forceinline__ float exact_distance16(const T* __restrict__ xr,
   // the scan's 16-B slots: 4 floats (f32) or 8 halves (f16), lane jl takes
   // slots jl, jl + 16, ... (knn_scan.hip plan_scan: W = 16 / sizeof(T))
   constexpr int W = 16 / sizeof(T);
+  constexpr int S = 16 * W;  // elements between a lane's slots
   typedef T vT __attribute__((ext_vector_type(W)));
+  typedef float vF __attribute__((ext_vector_type(W)));
   float acc = 0.f, acc2 = 0.f;
-  if (live) {
-    for (int k = jl * W; k < d; k += 16 * W) {
-      const vT xv = *reinterpret_cast<const vT*>(xr + k);
+  auto slot = [&](const vT& xv, const vF& yv) {
 #pragma unroll
-      for (int t = 0; t < W; ++t) {
-        const float x = (float)xv[t];
-        const float y = qv[k + t];
-        if constexpr (METRIC == 0) {
-          const float df = x - y;
-          acc = fmaf(df, df, acc);
-        } else if constexpr (METRIC == 1) {
-          acc = fmaf(x, y, acc);
-        } else {
-          acc = fmaf(x, y, acc);
-          acc2 = fmaf(x, x, acc2);
+    for (int t = 0; t < W; ++t) {
+      const float x = (float)xv[t];
+      const float y = yv[t];
+      if constexpr (METRIC == 0) {
+        const float df = x - y;
+        acc = fmaf(df, df, acc);
+      } else if constexpr (METRIC == 1) {
+        acc = fmaf(x, y, acc);
+      } else {
+        acc = fmaf(x, y, acc);
+        acc2 = fmaf(x, x, acc2);
+      }
+    }
+  };
+  // NS slots of the lane loaded at once (all of a 768-d f32 or a 1024-d f16
+  // row), then multiplied in the scan's order
+  constexpr int NS = W == 4 ? 12 : 8;
+  if (live) {
+    for (int base = jl * W; base < d; base += NS * S) {
+      vT xv[NS];
+      vF yv[NS];
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        const int k = base + i * S;
+        if (k < d) {
+          xv[i] = *reinterpret_cast<const vT*>(xr + k);
+          yv[i] = *reinterpret_cast<const vF*>(qv + k);
         }
       }
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        if (base + i * S < d) slot(xv[i], yv[i]);
     }
   }
   const float s1 = sum16(acc);  // the scan's reduction: bit-identical distances
@@ -331,10 +350,12 @@ __device__ __forceinline__ float exact_distance16(const T* __restrict__ xr,
   }
 }
 
-// Exact distance of each appended candidate (exact_distance16, 4 candidates
-// per wave); the key is replaced in place (row unchanged).  With thr, a
-// candidate whose (lower-bound) key is above the query's threshold key is
-// dropped unread.  Every lane of a wave runs the same number of iterations.
+// Exact distance of each appended candidate (exact_distance16); the key is
+// replaced in place (row unchanged).  With thr, a candidate whose
+// (lower-bound) key is above the query's threshold key is dropped (kEmpty)
+// unread.  Each wave takes 64 slots at a time, one per lane, and rescores the
+// kept ones 4 at a time (a 16-lane group each, the kept lanes taken in order
+// from the wave's ballot): dropped candidates cost one load and no group.
 template <typename T, int METRIC>
 __global__ void __launch_bounds__(256) rescore_kernel(const T* __restrict__ X, int64_t n, int d,
                                                       int64_t row_base,
@@ -344,25 +365,38 @@ __global__ void __launch_bounds__(256) rescore_kernel(const T* __restrict__ X, i
                                                       uint64_t* __restrict__ cand, int cap,
                                                       const uint64_t* __restrict__ thr) {
   const int64_t q = blockIdx.y;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int grp = lane >> 4, jl = lane & 15;
   const uint32_t cq = count[q * kCountStride];
-  const uint32_t cnt = cq < (uint32_t)cap ? cq : (uint32_t)cap;
+  const int64_t cnt = cq < (uint32_t)cap ? cq : (uint32_t)cap;
   const uint32_t tkey = thr != nullptr ? (uint32_t)(thr[q] >> 32) : 0xffffffffu;
   const float* qv = Q + q * (int64_t)d;
   const float qn = METRIC == 2 ? qnorm[q] : 0.f;
-  for (int64_t i0 = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 6) * 4; i0 < cnt;
-       i0 += (int64_t)gridDim.x * 16) {  // wave-uniform trip count
-    const int64_t i = i0 + grp;
-    uint64_t* slot = cand + q * (int64_t)cap + (i < cnt ? i : i0);
-    const uint64_t c = i < cnt ? *slot : kEmpty;
+  uint64_t* cl = cand + q * (int64_t)cap;
+  for (int64_t base = ((int64_t)blockIdx.x * 4 + wv) * 64; base < cnt;
+       base += (int64_t)gridDim.x * 256) {  // wave-uniform trip count
+    const int64_t i = base + lane;
+    const uint64_t c = i < cnt ? cl[i] : kEmpty;
     const int64_t row = (int64_t)(c & 0xffffffffull) - row_base;
-    const bool keep = c != kEmpty && (uint32_t)(c >> 32) <= tkey;
-    const bool live = keep && row >= 0 && row < n;
-    const float dist =
-        exact_distance16<T, METRIC>(X + (live ? row : 0) * (int64_t)d, qv, d, jl, live, qn);
-    if (jl == 0 && i < cnt && c != kEmpty) {
-      *slot = live ? make_comp(dist, (uint32_t)(c & 0xffffffffull)) : kEmpty;
+    const bool keep = c != kEmpty && (uint32_t)(c >> 32) <= tkey && row >= 0 && row < n;
+    if (c != kEmpty && !keep) cl[i] = kEmpty;
+    uint64_t m = __ballot(keep);
+    while (m != 0ull) {  // wave-uniform: groups 0..3 take the next 4 kept lanes
+      int src = -1;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int l = m != 0ull ? __builtin_ctzll(m) : -1;
+        if (m != 0ull) m &= m - 1ull;
+        if (g == grp) src = l;
+      }
+      const int from = src >= 0 ? src : 0;
+      const uint32_t lo = __shfl((uint32_t)c, from), hi = __shfl((uint32_t)(c >> 32), from);
+      const uint64_t cs = ((uint64_t)hi << 32) | lo;
+      const int64_t rs = (int64_t)lo - row_base;
+      const bool live = src >= 0;
+      const float dist =
+          exact_distance16<T, METRIC>(X + (live ? rs : 0) * (int64_t)d, qv, d, jl, live, qn);
+      if (jl == 0 && live) cl[base + src] = make_comp(dist, (uint32_t)(cs & 0xffffffffull));
     }
   }
 }
@@ -371,47 +405,44 @@ __global__ void __launch_bounds__(256) rescore_kernel(const T* __restrict__ X, i
 // [nq][k], run_merge's out_row, -1 = missing): their exact distances
 // (exact_distance16) are k rows' scan distances, so the largest composite
 // bounds the k-th smallest from above; thr[q] = min(thr[q], it).  A query
-// with fewer than k candidates keeps its threshold.  One block per query.
+// with fewer than k candidates keeps its threshold (a missing row counts as
+// the largest composite).  Grid (ceil(k / 16), nq): 16 rows per block, one
+// per 16-lane group; the blocks of a query fold into scratch[q] = {max,
+// ticket} and the last one to finish writes thr and re-zeroes the scratch.
 template <typename T, int METRIC>
 __global__ void __launch_bounds__(256) exact_kth_kernel(const T* __restrict__ X, int64_t n, int d,
                                                         int64_t row_base,
                                                         const float* __restrict__ Q,
                                                         const float* __restrict__ qnorm, int k,
                                                         const int64_t* __restrict__ rows,
-                                                        uint64_t* __restrict__ thr) {
+                                                        uint64_t* __restrict__ thr,
+                                                        unsigned long long* __restrict__ scratch) {
   __shared__ unsigned long long smax;
-  __shared__ int sbad;
-  const int64_t q = blockIdx.x;
-  const int lane = threadIdx.x & 63;
-  const int grp = (threadIdx.x >> 4), jl = lane & 15;  // 16 groups of 16 lanes
-  if (threadIdx.x == 0) {
-    smax = 0ull;
-    sbad = 0;
-  }
+  const int64_t q = blockIdx.y;
+  const int grp = threadIdx.x >> 4, jl = threadIdx.x & 15;
+  if (threadIdx.x == 0) smax = 0ull;
   __syncthreads();
-  const float* qv = Q + q * (int64_t)d;
+  const int j = blockIdx.x * 16 + grp;
+  const int64_t grow = j < k ? rows[q * (int64_t)k + j] : 0;
+  const int64_t row = grow - row_base;
+  const bool live = j < k && grow >= 0 && row >= 0 && row < n;
   const float qn = METRIC == 2 ? qnorm[q] : 0.f;
-  uint64_t mx = 0ull;
-  bool bad = false;
-  for (int j0 = 0; j0 < k; j0 += 16) {  // block-uniform trip count
-    const int j = j0 + grp;
-    const int64_t grow = j < k ? rows[q * (int64_t)k + j] : 0;
-    const int64_t row = grow - row_base;
-    const bool live = j < k && grow >= 0 && row >= 0 && row < n;
-    if (j < k && !live) bad = true;
-    const float dist =
-        exact_distance16<T, METRIC>(X + (live ? row : 0) * (int64_t)d, qv, d, jl, live, qn);
-    if (live) {
-      const uint64_t c = make_comp(dist, (uint32_t)grow);
-      mx = c > mx ? c : mx;
+  const float dist = exact_distance16<T, METRIC>(X + (live ? row : 0) * (int64_t)d,
+                                                 Q + q * (int64_t)d, d, jl, live, qn);
+  if (jl == 0 && j < k) atomicMax(&smax, live ? (unsigned long long)make_comp(dist, (uint32_t)grow)
+                                              : ~0ull);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long* sc = scratch + 2 * q;
+    atomicMax(&sc[0], smax);
+    __threadfence();
+    if (atomicAdd(&sc[1], 1ull) == gridDim.x - 1) {  // the query's last block
+      const unsigned long long m = atomicMax(&sc[0], 0ull);
+      if (m < thr[q]) thr[q] = m;
+      sc[0] = 0ull;
+      sc[1] = 0ull;
     }
   }
-  if (jl == 0) {
-    if (bad) atomicOr(&sbad, 1);
-    atomicMax(&smax, (unsigned long long)mx);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && sbad == 0 && smax < thr[q]) thr[q] = smax;
 }
 
 template <typename T>
@@ -436,8 +467,10 @@ int launch_rescore(const void* X, int dtype, int64_t n, int d, int64_t row_base,
   int cus = 0;
   int rc = device_cus(&cus);
   if (rc) return rc;
-  int64_t bx = ((int64_t)cap + 15) / 16;
-  if (bx > cus) bx = cus;
+  // enough blocks for ~8 per CU over the batch, at most one per 256 slots
+  int64_t bx = ((int64_t)cus * 8 + nq - 1) / (nq > 0 ? nq : 1);
+  if (bx > ((int64_t)cap + 255) / 256) bx = ((int64_t)cap + 255) / 256;
+  if (bx < 1) bx = 1;
   for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
     const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
     const dim3 grid((unsigned)bx, (unsigned)qn);
@@ -461,32 +494,33 @@ int launch_rescore(const void* X, int dtype, int64_t n, int d, int64_t row_base,
 template <typename T>
 static void launch_exact_kth_t(const T* X, int64_t n, int d, int64_t row_base, const float* Q,
                                const float* qnm, int k, const int64_t* rows, uint64_t* thr,
-                               int metric, dim3 grid, hipStream_t stream) {
+                               unsigned long long* sc, int metric, dim3 grid, hipStream_t stream) {
   if (metric == FX_METRIC_COS) {
     hipLaunchKernelGGL((exact_kth_kernel<T, 2>), grid, dim3(256), 0, stream, X, n, d, row_base,
-                       Q, qnm, k, rows, thr);
+                       Q, qnm, k, rows, thr, sc);
   } else if (metric == FX_METRIC_IP) {
     hipLaunchKernelGGL((exact_kth_kernel<T, 1>), grid, dim3(256), 0, stream, X, n, d, row_base,
-                       Q, qnm, k, rows, thr);
+                       Q, qnm, k, rows, thr, sc);
   } else {
     hipLaunchKernelGGL((exact_kth_kernel<T, 0>), grid, dim3(256), 0, stream, X, n, d, row_base,
-                       Q, qnm, k, rows, thr);
+                       Q, qnm, k, rows, thr, sc);
   }
 }
 
 int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_base,
                      const float* Q, const float* qnorm, int64_t nq, int k, const int64_t* rows,
-                     int metric, uint64_t* thr, hipStream_t stream) {
+                     int metric, uint64_t* thr, uint64_t* scratch, hipStream_t stream) {
+  auto* sc = reinterpret_cast<unsigned long long*>(scratch);
   for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
     const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
-    const dim3 grid((unsigned)qn);
+    const dim3 grid((unsigned)((k + 15) / 16), (unsigned)qn);
     const float* qnm = qnorm != nullptr ? qnorm + q0 : nullptr;
     if (dtype == FX_DTYPE_F16) {
       launch_exact_kth_t(reinterpret_cast<const _Float16*>(X), n, d, row_base, Q + q0 * d, qnm, k,
-                         rows + q0 * k, thr + q0, metric, grid, stream);
+                         rows + q0 * k, thr + q0, sc + 2 * q0, metric, grid, stream);
     } else {
       launch_exact_kth_t(reinterpret_cast<const float*>(X), n, d, row_base, Q + q0 * d, qnm, k,
-                         rows + q0 * k, thr + q0, metric, grid, stream);
+                         rows + q0 * k, thr + q0, sc + 2 * q0, metric, grid, stream);
     }
     int rc = check_launch("exact_kth_kernel");
     if (rc) return rc;

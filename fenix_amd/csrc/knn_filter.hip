@@ -1151,13 +1151,15 @@ static int launch_img2(const FilterArgs& a, int metric, hipStream_t stream) {
 #define FX_I3_QA 3   // query chunks in flight (ring of FX_I3_QA + 1 slots)
 #endif
 #ifndef FX_I3_XS
-#define FX_I3_XS 2   // image chunks in flight per wave (register stages)
+#define FX_I3_XS 4   // image chunks in flight per wave (register stages; 2 and 3
+                     // measured 1-2 % slower, tools/ab_i8x.sh)
 #endif
 #ifndef FX_I3_SEG
 #define FX_I3_SEG 24  // LDS append entries per query (overflow: global slots)
 #endif
 #ifndef FX_I3_XPF
-#define FX_I3_XPF 1   // the next tile's first image chunks in flight during the epilogue
+#define FX_I3_XPF 0   // 1: the next tile's first image chunks in flight during the
+                      // epilogue (equal with 4 stages, 1-2 % faster with 2)
 #endif
 constexpr int kI3Slots = FX_I3_QA + 1;
 constexpr int kI3QBytes = fBQ * fBK * 2;               // one slot: 16 KB
@@ -1374,44 +1376,49 @@ __device__ __forceinline__ void i8_query_table(const FilterArgs& a, int64_t q0, 
   }
 }
 
-// [lb, ub] of an appended (row, query) pair of the int8 filter, in double,
-// rounded outward: M the accumulator, the row's {omega, y1, 1/s}
-// (i8_note_row) and the query's launch_qprep8 record.
+// [lb, ub] of an appended (row, query) pair of the int8 filter from M, the
+// row's {omega, y1, 1/s} (i8_note_row) and the query's launch_qprep8 record,
+// in f32 with outward slack: every rounding below is relative to a term it
+// is added to (at most ~8 u each), so each bound is widened by 16 u of the
+// magnitudes it was computed from.
 template <int METRIC>
 __device__ __forceinline__ void i8_bounds(float m, float om, float y1, float is, f32x4 qi, int d,
-                                       float& lb, float& ub) {
+                                          float& lb, float& ub) {
   if (om != om) {  // forced row: below / above every key
     lb = -__builtin_inff();
     ub = __builtin_nanf("");
     return;
   }
-  const double u = 5.9604644775390625e-08;
-  const double g = (double)(d + 2) * u * 1.01;
-  const double I = (double)(m - kI8Magic);  // exact
-  const double E = (double)om * (double)qi[1] * (1.0 + 1e-6) + 4.0;
-  const double s = 1.0 / (double)is;  // (1/s was rounded: relative slack below)
-  const double sig = s * (double)qi[0] * (1.0 + 1e-6);
-  double lo, hi;
+  const float u = 5.9604644775390625e-08f;
+  const float g = (float)(d + 2) * u * 1.01f;
+  const float I = m - kI8Magic;  // exact
+  const float E = fmaf(om * qi[1], 8.f * u, om * qi[1]) + 4.f;
+  const float s = 1.f / is;
+  const float sig = s * qi[0];
+  const float a1 = I + E, a2 = I - E;
   if constexpr (METRIC == 1) {
-    lo = -sig * (I + E);
-    hi = -sig * (I - E);
+    const float lo = -sig * a1, hi = -sig * a2;
+    lb = lo - 16.f * u * fabsf(lo);
+    ub = hi + 16.f * u * fabsf(hi);
   } else if constexpr (METRIC == 2) {
-    const double c = 3.0 * g + 32.0 * u;
-    const double den = fmax((double)y1 * s, 1e-12) * fmax((double)qi[3], 1e-12);
-    lo = 0.5 - 0.5 * sig * (I + E) / den - c;
-    hi = 0.5 - 0.5 * sig * (I - E) / den + c;
+    const float c = 3.f * g + 32.f * u;
+    const float den = fmaxf(y1 * s, 1e-12f) * fmaxf(qi[3], 1e-12f);
+    const float r1 = sig * a1 / den, r2 = sig * a2 / den;
+    lb = 0.5f - 0.5f * r1 - c - 16.f * u * (1.f + fabsf(r1));
+    ub = 0.5f - 0.5f * r2 + c + 16.f * u * (1.f + fabsf(r2));
   } else {
-    const double g2 = 2.0 * g + 8.0 * u;
-    const double n2 = (double)y1 * s;
-    const double alo = n2 * (1.0 - g - 16.0 * u) + (double)qi[2] * (1.0 - 4.0 * u);
-    const double ahi = n2 * (1.0 + g + 16.0 * u) + (double)qi[2] * (1.0 + 4.0 * u);
-    lo = sqrt(fmax((1.0 - g2) * (alo - 2.0 * sig * (I + E)), 0.0));
-    hi = sqrt(fmax((1.0 + g2) * (ahi - 2.0 * sig * (I - E)), 0.0));
+    const float g2 = 2.f * g + 8.f * u;
+    const float n2 = y1 * s;
+    const float alo = n2 * (1.f - g - 16.f * u) + qi[2] * (1.f - 4.f * u);
+    const float ahi = n2 * (1.f + g + 16.f * u) + qi[2] * (1.f + 4.f * u);
+    const float t1 = 2.f * sig * a1, t2 = 2.f * sig * a2;
+    const float lo2 = (1.f - g2) * (alo - t1) - 16.f * u * (alo + fabsf(t1));
+    const float hi2 = (1.f + g2) * (ahi - t2) + 16.f * u * (ahi + fabsf(t2));
+    lb = sqrtf(fmaxf(lo2, 0.f)) * (1.f - 4.f * u);
+    ub = sqrtf(fmaxf(hi2, 0.f)) * (1.f + 4.f * u);
   }
-  lb = __double2float_rd(lo);
-  ub = __double2float_ru(hi);
-  if (lo != lo) lb = -__builtin_inff();  // (a non-finite query: R' = inf)
-  if (hi != hi) ub = __builtin_nanf("");
+  if (lb != lb) lb = -__builtin_inff();  // (a non-finite query: R' = inf)
+  if (ub != ub) ub = __builtin_nanf("");
 }
 
 // One row's values for the int8 epilogue: omega (NaN: forced), y1 and 1/s,
@@ -1480,6 +1487,38 @@ __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const fl
   for (int u = 0; u < kI2QT; ++u) {
     pm[u] = (diag & 1) ? 0u : (~fail[u] | fmask) & ~smask & 0xffffu;
     if (q0 + u * 32 + l32 >= a.nq) pm[u] = 0u;
+  }
+  if (a.all_pass) {  // no threshold yet (first phase): every live pair, slots reserved
+                     // per lane and query, accumulators indexed statically
+    static_for<kI2QT>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      const uint32_t bits = pm[u];
+      if (__ballot(bits != 0u) == 0ull) return;
+      const int qi = u * 32 + (int)opaque((unsigned)l32);
+      const int64_t gq = q0 + qi;
+      uint32_t p = bits != 0u ? atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(bits)) : 0u;
+      const f32x4 qrec = qinf[qi];
+      static_for<16>([&](auto jc) {
+        constexpr int jj = decltype(jc)::value;
+        if (!((bits >> jj) & 1u)) return;
+        // (opaque: 16 rows' LDS offsets hoisted to the kernel start were spilled)
+        const int lr = (int)opaque((unsigned)lr0) + (jj & 3) + 8 * (jj >> 2);
+        float lb, ub;
+        i8_bounds<METRIC>(acc[u][jj], rinfo[lr], rterm[lr], rext[lr], qrec, a.d, lb, ub);
+        if (p < (uint32_t)a.cap) {
+          const uint32_t grow = (uint32_t)(a.row_base + r0) + (uint32_t)lr;
+          const size_t slot = (size_t)gq * a.cap + p;
+          if (a.cand_ub != nullptr) {
+            a.cand[slot] = make_comp(lb, grow);
+            a.cand_ub[slot] = make_comp(ub, grow);
+          } else {
+            a.cand[slot] = make_comp(ub, grow);
+          }
+        }
+        ++p;
+      });
+    });
+    return;
   }
   uint32_t any = 0u;
 #pragma unroll

@@ -26,7 +26,8 @@ __global__ void __launch_bounds__(kMergeThreads)
     merge_kernel(const uint64_t* __restrict__ in, int64_t nlists, int kin, int64_t G, int k,
                  int P2, uint64_t* __restrict__ out_lists, float* __restrict__ out_dist,
                  int64_t* __restrict__ out_row, uint64_t* __restrict__ out_kth,
-                 int final_level, const uint32_t* __restrict__ gate, int64_t gate_cap) {
+                 int final_level, const uint32_t* __restrict__ gate, int64_t gate_cap,
+                 const uint32_t* __restrict__ count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   MergeShared* ms = reinterpret_cast<MergeShared*>(smem);
   uint64_t* res = reinterpret_cast<uint64_t*>(smem + sizeof(MergeShared));
@@ -39,7 +40,13 @@ __global__ void __launch_bounds__(kMergeThreads)
   if (gate != nullptr && (int64_t)gate[(size_t)q * kCountStride] <= gate_cap) return;
   const int64_t l0 = (int64_t)blockIdx.x * G;
   const int nl = (int)((nlists - l0) < G ? (nlists - l0) : G);
-  const int m = nl * kin;
+  int m = nl * kin;
+  if (count != nullptr) {  // appended lists: only the first count[q] slots hold entries
+    const int64_t c = (int64_t)count[(size_t)q * kCountStride];
+    const int64_t all = nlists * kin;
+    const int64_t valid = (c < all ? c : all) - l0 * kin;
+    m = valid < 0 ? 0 : (valid < m ? (int)valid : m);
+  }
   const uint64_t* src = in + ((size_t)q * nlists + l0) * (size_t)kin;
   block_reset(ms);
   __syncthreads();
@@ -173,7 +180,7 @@ int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p)
 
 int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, void* ws,
               float* out_dist, int64_t* out_row, hipStream_t stream, uint64_t* out_kth,
-              const uint32_t* gate, int64_t gate_cap) {
+              const uint32_t* gate, int64_t gate_cap, const uint32_t* count) {
   const int P2 = next_pow2((int)k);
   uint64_t* bufs[2] = {reinterpret_cast<uint64_t*>(ws),
                        reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + p.ws_bytes / 2)};
@@ -197,8 +204,11 @@ int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, voi
       int64_t* orow = out_row ? out_row + (size_t)q0 * k : nullptr;
       uint64_t* okth = out_kth ? out_kth + q0 : nullptr;
       const uint32_t* gq = gate ? gate + (size_t)q0 * kCountStride : nullptr;
+      const uint32_t* cq = count != nullptr && lv == 0 ? count + (size_t)q0 * kCountStride
+                                                       : nullptr;
       hipLaunchKernelGGL(merge_kernel, grid, dim3(kMergeThreads), smem, stream, src, lists,
-                         (int)klen, G, (int)k, P2, dq, od, orow, okth, fin ? 1 : 0, gq, gate_cap);
+                         (int)klen, G, (int)k, P2, dq, od, orow, okth, fin ? 1 : 0, gq, gate_cap,
+                         cq);
       int rc = check_launch("merge_kernel");
       if (rc) return rc;
     }

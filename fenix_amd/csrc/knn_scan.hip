@@ -902,6 +902,17 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   return FX_OK;
 }
 
+void limit_scan_blocks(ScanPlan* p, int64_t n, int64_t max_blocks) {
+  if (max_blocks < 1 || p->blocks <= max_blocks) return;
+  const int64_t step = 16 * (int64_t)p->U;
+  int64_t rpb = (n + max_blocks - 1) / max_blocks;
+  rpb = (rpb + step - 1) / step * step;
+  p->rows_per_block = rpb > 0 ? rpb : step;
+  p->blocks = (n + p->rows_per_block - 1) / p->rows_per_block;
+  if (p->blocks < 1) p->blocks = 1;
+  p->nlists = p->blocks;
+}
+
 int launch_scan(const ScanPlan& p, const ScanArgs& a, int64_t nq, hipStream_t stream) {
   dim3 grid((unsigned)p.blocks, (unsigned)nq);
   if (p.fn_dma != nullptr && a.mask == nullptr && a.rows == nullptr) {
