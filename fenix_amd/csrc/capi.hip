@@ -710,10 +710,10 @@ static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_
       }
       if (img && img8) {  // int8 image: denser samples (filter_phases)
         BatchLayout b = s.batch;
-        int64_t r = b.cap / (4 * k);
-        if (r > kI8SampleRatio) r = kI8SampleRatio;
-        const int64_t v = option(kOptBatchRatio);
-        if (v >= 2 && v < r) r = v;
+        const int64_t rmax = b.cap / (4 * k);
+        int64_t r = rmax < kI8SampleRatio ? rmax : kI8SampleRatio;
+        const int64_t v = option(kOptBatchRatio);  // test switch: any ratio up to rmax
+        if (v >= 2) r = v < rmax ? v : rmax;
         rc = plan_phases(&b, filter_tile_rows(dtype), r);
         if (rc) return rc;
         return filter_phases(b, corpus, dtype, image, rowinfo, true, n, d, row_base, queries, nq,
