@@ -40,8 +40,8 @@ static std::mutex g_mu;
 // ----------------------------------------------------------------- options --
 static const char* const kOptNames[kOptCount] = {
     "batched", "batch_min_queries", "batch_cap", "batch_sample_ratio",
-    "force_fallback", "scan_interleave", "q8_dma", "filter_image"};
-static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}, {8}};
+    "force_fallback", "scan_interleave", "q8_dma", "filter_image", "batch_ub_test"};
+static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}, {8}, {1}};
 
 int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
 
@@ -485,6 +485,11 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
     a.qstride = img8 ? nq_pad8 : b.nq_pad;
     a.img8 = img8 ? 1 : 0;
     a.all_pass = ph == 0 ? 1 : 0;  // (thr was just filled with the empty key)
+    // sampling phases need only the k smallest upper bounds of their rows:
+    // the k rows behind the previous threshold are in this (nested) sample
+    // with upper bounds at or below it, so no row whose upper bound exceeds
+    // it is among them (option "batch_ub_test" = 0: the lower-bound test)
+    a.ub_test = ph > 0 && !last && option(kOptBatchUbTest) != 0 ? 1 : 0;
     a.qinfo = qinfo;
     a.nq = nq;
     a.mask = mask;

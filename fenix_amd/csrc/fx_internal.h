@@ -22,6 +22,7 @@ enum Option : int {
   kOptScanInterleave,
   kOptQ8Dma,
   kOptFilterImage,  // filter image bits for f32 corpora (engine policy): 8, 16 or 0 (none)
+  kOptBatchUbTest,  // sampling phases append by upper bound (0: by lower bound, test switch)
   kOptCount
 };
 int64_t option(Option o);
@@ -163,6 +164,8 @@ struct FilterArgs {
                           // launch_qprep8
   int all_pass;           // no query has a threshold yet (thr all empty): img8 appends
                           // every live pair without the test
+  int ub_test;            // sampling phase after the first: append when the UPPER bound
+                          // reaches the threshold (only the k-th upper bound is needed)
   int diag;               // FX_FILTER_DIAG (diagnostic builds only): 1 no appends, 2 no epilogue,
                           // 4 no MFMA, 8 no query loads, 16 no LDS stores,
                           // 32 no append atomics, 64 no append stores

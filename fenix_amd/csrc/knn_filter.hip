@@ -343,26 +343,31 @@ __device__ __forceinline__ void filter_query_table(const FilterArgs& a, int64_t 
     float2 ab = {0.f, __builtin_inff()};
     if (gq < a.nq) {
       const f32x4 info = *reinterpret_cast<const f32x4*>(a.qinfo + gq * 4);
-      const float tf = key_float((uint32_t)(a.thr[gq] >> 32));
+      float tf = key_float((uint32_t)(a.thr[gq] >> 32));
       const float qinv = info[0], qa = info[1], qA = info[2], qB = info[3];
       c[2] = qA;
       c[3] = qB;
+      // the upper-bound test (ub_test): the same forms with the error terms
+      // A, B negated, and T widened by 2^-14 relative (the rows that set T
+      // pass again; extra passes only cost an append)
+      const float sA = a.ub_test ? -qA : qA, sB = a.ub_test ? -qB : qB;
+      if (a.ub_test) tf += fabsf(tf) * 6.103515625e-05f;
       if constexpr (METRIC == 0) {
         c[0] = -2.f * qinv;
         c[1] = qa;
         const float t2 = tf * tf * (1.f + 9.5367431640625e-07f);
         const float h = 0.5f / qinv;
-        ab.x = (1.f - qA) * h;
-        ab.y = ((1.f - qA) * qa - qB - t2) * h;
+        ab.x = (1.f - sA) * h;
+        ab.y = ((1.f - sA) * qa - sB - t2) * h;
       } else if constexpr (METRIC == 1) {
         c[0] = -qinv;
         const float sc = 1.f / qinv;
-        ab.x = -qA * sc;
-        ab.y = (-tf - qB) * sc;
+        ab.x = -sA * sc;
+        ab.y = (-tf - sB) * sc;
       } else {
         c[0] = -0.5f * qinv / qa;
-        ab.x = (tf - 0.5f + qA) / c[0];
-        ab.y = qB / c[0];
+        ab.x = (tf - 0.5f + sA) / c[0];
+        ab.y = sB / c[0];
       }
       if (tf != tf || !(qA <= 3.4e38f)) ab = {0.f, -__builtin_inff()};
     }
@@ -1351,7 +1356,10 @@ __device__ __forceinline__ void i8_query_table(const FilterArgs& a, int64_t q0, 
     f32x4 c = f32x4(0.f), qi = f32x4(0.f);
     if (gq < a.nq) {
       qi = *reinterpret_cast<const f32x4*>(a.qinfo + gq * kI8QInfo);  // {s_q, R', n_q^2, |q|}
-      const float tf = key_float((uint32_t)(a.thr[gq] >> 32));
+      float tf = key_float((uint32_t)(a.thr[gq] >> 32));
+      // the upper-bound test (ub_test): -R' below, T widened by 2^-14
+      // relative (the rows that set T pass again)
+      if (a.ub_test) tf += fabsf(tf) * 6.103515625e-05f;
       const float sq = qi[0];
       c[0] = qi[1];
       if constexpr (METRIC == 1) {
@@ -1369,7 +1377,10 @@ __device__ __forceinline__ void i8_query_table(const FilterArgs& a, int64_t q0, 
         c[1] = -L1 * (1.f - g - 16.f * u);
         c[2] = -L0 + 16.f * u * fabsf(L0);
       }
-      if (tf != tf || !(c[0] <= 3.4e38f)) c = f32x4{__builtin_inff(), 0.f, 0.f, 0.f};
+      if (tf != tf || !(c[0] <= 3.4e38f))
+        c = f32x4{__builtin_inff(), 0.f, 0.f, 0.f};
+      else if (a.ub_test)
+        c[0] = -c[0];
     }
     qtab[i] = c;
     qinf[i] = qi;

@@ -116,7 +116,9 @@ __global__ void __launch_bounds__(kMergeThreads)
   }
   uint64_t* sorted = res;
   res = sorted;
-  if (out_kth != nullptr && tid == 0) out_kth[q] = res[k - 1];
+  // (a threshold only tightens: a phase with fewer than k candidates, or
+  // whose k-th is above the previous one, keeps the previous)
+  if (out_kth != nullptr && tid == 0 && res[k - 1] < out_kth[q]) out_kth[q] = res[k - 1];
   if (out_dist == nullptr) return;
   for (int i = tid; i < k; i += kMergeThreads) {
     const uint64_t e = res[i];

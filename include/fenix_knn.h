@@ -81,8 +81,10 @@ int fx_device_count(int* out);
  * Test switches (they change which code runs, never the results):
  *   "batch_cap"           0  candidate buffer per query of the batched filter
  *                            (0: max(64 k, 16 K); smaller than 16 k is ignored)
- *   "batch_sample_ratio"  0  row-sample ratio of the filter phases (0: cap / 4k;
- *                            only denser samples are accepted)
+ *   "batch_sample_ratio"  0  row-sample ratio of the filter phases (0: cap / 4k,
+ *                            8 with an int8 image; up to cap / 4k accepted)
+ *   "batch_ub_test"       1  sampling phases append the pairs whose upper
+ *                            bound reaches the threshold (0: lower bound)
  *   "force_fallback"      0  1: every batched query is recomputed by the exact
  *                            single-query scan, as if its candidates overflowed
  *   "scan_interleave"    -1  -1: by row size; 0: one row range per workgroup;

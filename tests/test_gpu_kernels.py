@@ -497,9 +497,10 @@ def test_batched_filter_bit_identical_to_scan(eng, metric, n, d, nq, k):
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
 def test_batched_filter_sampling_plan_invariant(eng, dtype):
     """The nested sample phases only set thresholds: any candidate buffer size
-    and sample ratio ("batch_cap" / "batch_sample_ratio", e.g. 2-5 phases)
-    gives the same rows and distances, bit for bit (every kept candidate is
-    rescored)."""
+    and sample ratio ("batch_cap" / "batch_sample_ratio", e.g. 2-5 phases),
+    and either pass test of the sampling phases ("batch_ub_test": by upper or
+    lower bound), gives the same rows and distances, bit for bit (every kept
+    candidate is rescored)."""
     n, d, nq, k = 400_000, 256, 96, 50
     tdt = torch.float16 if dtype == "f16" else torch.float32
     x = gpu_fill(eng, n, d, seed=31, dtype=tdt)
@@ -508,8 +509,9 @@ def test_batched_filter_sampling_plan_invariant(eng, dtype):
         q = q.astype(np.float16).astype(np.float32)
     for metric in METRICS:
         base_d, base_r = gpu_search(eng, x, q, metric, k)
-        for cap, r in ((0, 3), (0, 8), (32768, 0), (16 * k, 2)):
-            with _lib.options(batch_cap=cap, batch_sample_ratio=r):
+        for cap, r, ub in ((0, 3, 1), (0, 8, 1), (32768, 0, 1), (16 * k, 2, 1), (0, 0, 0),
+                           (16 * k, 2, 0), (0, 12, 0)):
+            with _lib.options(batch_cap=cap, batch_sample_ratio=r, batch_ub_test=ub):
                 pd, pr = gpu_search(eng, x, q, metric, k)
             np.testing.assert_array_equal(pr, base_r)
             np.testing.assert_array_equal(pd.view(np.uint32), base_d.view(np.uint32))
