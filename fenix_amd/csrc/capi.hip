@@ -200,7 +200,7 @@ struct BatchLayout {
   int64_t start[16], stride[16], num[16];
   MergePlan merge;
   size_t off_qnorm, off_thr, off_count, off_cand, off_merge, off_cand_ub, off_qh, off_qinfo,
-      off_topd, off_topr, off_kmax, total;
+      off_topd, off_topr, total;
 };
 
 // The fp16-MFMA filter (knn_filter.hip).  Diagnostic builds keep the
@@ -269,8 +269,6 @@ static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, 
     off += align256((size_t)nq * k * 4);
     b->off_topr = off;
     off += align256((size_t)nq * k * 8);
-    b->off_kmax = off;  // launch_exact_kth's per-query maxima and block tickets
-    off += align256((size_t)nq * 16);
   }
   b->total = off;
   return FX_OK;
@@ -467,7 +465,6 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
     if (rc) return rc;
   }
   hipError_t e = hipMemsetAsync(thr, 0xFF, (size_t)nq * 8, st);
-  if (img8 && e == hipSuccess) e = hipMemsetAsync(w + b.off_kmax, 0, (size_t)nq * 16, st);
   for (int ph = 0; ph < b.nphases && e == hipSuccess; ++ph) {
     const bool last = ph + 1 == b.nphases;
     // (the lists are read up to count only: no fill of the candidate buffers)
@@ -514,7 +511,7 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
                      nullptr, nullptr, 0, count);
       if (rc) return rc;
       rc = launch_exact_kth(X, dtype, n, (int)d, row_base, Q, qnorm, nq, (int)k, topr, metric,
-                            thr, reinterpret_cast<uint64_t*>(w + b.off_kmax), st);
+                            thr, st);
       if (rc) return rc;
       continue;
     }

@@ -133,8 +133,8 @@ int launch_rescore(const void* X, int dtype, int64_t n, int d, int64_t row_base,
 // [nq][k] (global, -1 = missing: the query keeps its threshold)); scratch
 // [nq][2] uint64 zeroed before the first call (left zeroed by each call)
 int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_base,
-                     const float* Q, const float* qnorm, int64_t nq, int k, const int64_t* rows,
-                     int metric, uint64_t* thr, uint64_t* scratch, hipStream_t stream);
+                     const float* Q, const float* qnorm, int64_t nq, int k, int64_t* rows,
+                     int metric, uint64_t* thr, hipStream_t stream);
 
 // Batched filter on the fp16 matrix cores (knn_filter.hip): appends every
 // (row, query) whose rigorous lower bound reaches the query's threshold.

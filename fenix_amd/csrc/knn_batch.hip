@@ -404,24 +404,22 @@ __global__ void __launch_bounds__(256) rescore_kernel(const T* __restrict__ X, i
 // Exact threshold from a query's k best candidates by upper bound (rows
 // [nq][k], run_merge's out_row, -1 = missing): their exact distances
 // (exact_distance16) are k rows' scan distances, so the largest composite
-// bounds the k-th smallest from above; thr[q] = min(thr[q], it).  A query
-// with fewer than k candidates keeps its threshold (a missing row counts as
-// the largest composite).  Grid (ceil(k / 16), nq): 16 rows per block, one
-// per 16-lane group; the blocks of a query fold into scratch[q] = {max,
-// ticket} and the last one to finish writes thr and re-zeroes the scratch.
+// bounds the k-th smallest from above; thr[q] = min(thr[q], it).  Two
+// launches: exact_kth_kernel replaces each row in place by its exact
+// composite (a missing row by the largest composite, so a query with fewer
+// than k candidates keeps its threshold), grid (ceil(k / 16), nq), one row
+// per 16-lane group; kth_max_kernel folds a query's k composites, one wave
+// per query.  (One launch with a per-query block ticket behind a
+// __threadfence took ~100 us for 256 x 100 rows: the blocks' fences and
+// returning atomics, not the row loads, set its time.)
 template <typename T, int METRIC>
 __global__ void __launch_bounds__(256) exact_kth_kernel(const T* __restrict__ X, int64_t n, int d,
                                                         int64_t row_base,
                                                         const float* __restrict__ Q,
                                                         const float* __restrict__ qnorm, int k,
-                                                        const int64_t* __restrict__ rows,
-                                                        uint64_t* __restrict__ thr,
-                                                        unsigned long long* __restrict__ scratch) {
-  __shared__ unsigned long long smax;
+                                                        int64_t* __restrict__ rows) {
   const int64_t q = blockIdx.y;
   const int grp = threadIdx.x >> 4, jl = threadIdx.x & 15;
-  if (threadIdx.x == 0) smax = 0ull;
-  __syncthreads();
   const int j = blockIdx.x * 16 + grp;
   const int64_t grow = j < k ? rows[q * (int64_t)k + j] : 0;
   const int64_t row = grow - row_base;
@@ -429,20 +427,23 @@ __global__ void __launch_bounds__(256) exact_kth_kernel(const T* __restrict__ X,
   const float qn = METRIC == 2 ? qnorm[q] : 0.f;
   const float dist = exact_distance16<T, METRIC>(X + (live ? row : 0) * (int64_t)d,
                                                  Q + q * (int64_t)d, d, jl, live, qn);
-  if (jl == 0 && j < k) atomicMax(&smax, live ? (unsigned long long)make_comp(dist, (uint32_t)grow)
-                                              : ~0ull);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long* sc = scratch + 2 * q;
-    atomicMax(&sc[0], smax);
-    __threadfence();
-    if (atomicAdd(&sc[1], 1ull) == gridDim.x - 1) {  // the query's last block
-      const unsigned long long m = atomicMax(&sc[0], 0ull);
-      if (m < thr[q]) thr[q] = m;
-      sc[0] = 0ull;
-      sc[1] = 0ull;
-    }
+  if (jl == 0 && j < k)
+    rows[q * (int64_t)k + j] = live ? (int64_t)make_comp(dist, (uint32_t)grow) : (int64_t)kEmpty;
+}
+
+__global__ void __launch_bounds__(256) kth_max_kernel(const uint64_t* __restrict__ comps,
+                                                      int64_t nq, int k,
+                                                      uint64_t* __restrict__ thr) {
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (q >= nq) return;
+  uint64_t m = 0ull;
+  for (int j = lane; j < k; j += 64) {
+    const uint64_t c = comps[q * (int64_t)k + j];
+    m = c > m ? c : m;
   }
+  m = wave_max_u64(m);
+  if (lane == 0 && m < thr[q]) thr[q] = m;
 }
 
 template <typename T>
@@ -493,39 +494,40 @@ int launch_rescore(const void* X, int dtype, int64_t n, int d, int64_t row_base,
 
 template <typename T>
 static void launch_exact_kth_t(const T* X, int64_t n, int d, int64_t row_base, const float* Q,
-                               const float* qnm, int k, const int64_t* rows, uint64_t* thr,
-                               unsigned long long* sc, int metric, dim3 grid, hipStream_t stream) {
+                               const float* qnm, int k, int64_t* rows, int metric, dim3 grid,
+                               hipStream_t stream) {
   if (metric == FX_METRIC_COS) {
     hipLaunchKernelGGL((exact_kth_kernel<T, 2>), grid, dim3(256), 0, stream, X, n, d, row_base,
-                       Q, qnm, k, rows, thr, sc);
+                       Q, qnm, k, rows);
   } else if (metric == FX_METRIC_IP) {
     hipLaunchKernelGGL((exact_kth_kernel<T, 1>), grid, dim3(256), 0, stream, X, n, d, row_base,
-                       Q, qnm, k, rows, thr, sc);
+                       Q, qnm, k, rows);
   } else {
     hipLaunchKernelGGL((exact_kth_kernel<T, 0>), grid, dim3(256), 0, stream, X, n, d, row_base,
-                       Q, qnm, k, rows, thr, sc);
+                       Q, qnm, k, rows);
   }
 }
 
 int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_base,
-                     const float* Q, const float* qnorm, int64_t nq, int k, const int64_t* rows,
-                     int metric, uint64_t* thr, uint64_t* scratch, hipStream_t stream) {
-  auto* sc = reinterpret_cast<unsigned long long*>(scratch);
+                     const float* Q, const float* qnorm, int64_t nq, int k, int64_t* rows,
+                     int metric, uint64_t* thr, hipStream_t stream) {
   for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
     const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
     const dim3 grid((unsigned)((k + 15) / 16), (unsigned)qn);
     const float* qnm = qnorm != nullptr ? qnorm + q0 : nullptr;
     if (dtype == FX_DTYPE_F16) {
       launch_exact_kth_t(reinterpret_cast<const _Float16*>(X), n, d, row_base, Q + q0 * d, qnm, k,
-                         rows + q0 * k, thr + q0, sc + 2 * q0, metric, grid, stream);
+                         rows + q0 * k, metric, grid, stream);
     } else {
       launch_exact_kth_t(reinterpret_cast<const float*>(X), n, d, row_base, Q + q0 * d, qnm, k,
-                         rows + q0 * k, thr + q0, sc + 2 * q0, metric, grid, stream);
+                         rows + q0 * k, metric, grid, stream);
     }
     int rc = check_launch("exact_kth_kernel");
     if (rc) return rc;
   }
-  return FX_OK;
+  hipLaunchKernelGGL(kth_max_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, stream,
+                     reinterpret_cast<const uint64_t*>(rows), nq, k, thr);
+  return check_launch("kth_max_kernel");
 }
 
 }  // namespace fx

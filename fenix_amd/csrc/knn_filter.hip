@@ -1693,28 +1693,39 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
     bq[s] = (uint32_t)(Q * 64 + (((2 * s + h) ^ ((Q >> 2) & 3)) * 16));
   }
   f32x16 acc[kI2QT];
-  auto compute = [&](const XA& xa, int slot) {
+  // a tile's first k-step takes its accumulator input from this constant
+  // (int8: the bits of 1.5 * 2^23, see "int8 filter image"; fp16: zeros)
+  // instead of 128 moves per tile into the accumulators
+  const f32x16 acc0 = f32x16(I8 ? kI8Magic : 0.f);
+  // FIRST: the tile's first chunk (its k-step 0 starts from acc0)
+  auto compute = [&](const XA& xa, int slot, auto first) {
+    constexpr bool FIRST = decltype(first)::value;
     if (diag & 4) {  // (diagnostics: no MFMA; the row loads stay live)
       if (xa[0][0] == (_Float16)1.2345f && xa[kI2KS - 1][7] == (_Float16)2.f) a.count[0] = 7;
+      if (FIRST) {
+#pragma unroll
+        for (int u = 0; u < kI2QT; ++u) acc[u] = acc0;
+      }
       return;
     }
     const unsigned char* st = sh->qring[slot];
-#pragma unroll
-    for (int s = 0; s < kI2KS; ++s) {
+    static_for<kI2KS>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
 #pragma unroll
       for (int u = 0; u < kI2QT; ++u) {
         // (query tile u sits 32 x 64 B further: (Q + 32 u) has the same swizzle)
         const f16x8 bv = *reinterpret_cast<const f16x8*>(st + bq[s] + u * 32 * 64);
+        const f32x16 cin = (FIRST && s == 0) ? acc0 : acc[u];
         if constexpr (I8) {
           typedef int i32x16 __attribute__((ext_vector_type(16)));
           acc[u] = __builtin_bit_cast(f32x16, __builtin_amdgcn_mfma_i32_32x32x32_i8(
               __builtin_bit_cast(i32x4, xa[s]), __builtin_bit_cast(i32x4, bv),
-              __builtin_bit_cast(i32x16, acc[u]), 0, 0, 0));
+              __builtin_bit_cast(i32x16, cin), 0, 0, 0));
         } else {
-          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bv, acc[u], 0, 0, 0);
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bv, cin, 0, 0, 0);
         }
       }
-    }
+    });
   };
 
   // ---- prologue: query chunks 0 .. QA-1 and image chunks 0 .. XS-1 of the
@@ -1745,14 +1756,12 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
   for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
     const int64_t r0 = (a.tile_start + ti * a.tile_stride) * fBM;
     if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;  // (read two tiles back)
-#pragma unroll
-    for (int u = 0; u < kI2QT; ++u) acc[u] = f32x16(I8 ? kI8Magic : 0.f);
     std::conditional_t<I8, f32x4, float> rsum = {};
     uint32_t mword = 0u;
     // one K step: multiply chunk c + S, then (LOAD) refill its register
     // stage with the chunk XS steps ahead (the next tile's first chunks at
     // the end of a tile, FX_I3_XPF)
-    auto step = [&](int c, auto sc, auto ld) {
+    auto step = [&](int c, auto sc, auto ld, auto first) {
       constexpr int S = decltype(sc)::value;
       // query chunk c + S landed (this wave's DMAs; the loads issued after
       // it: the image chunk of its step, then QA - 1 steps of both), and
@@ -1764,7 +1773,7 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
       issue_q(qc, qslot);
       qc = qc + 1 == nch ? 0 : qc + 1;
       qslot = qslot + 1 == kI3Slots ? 0 : qslot + 1;
-      if (S == 0 && c == 0) {  // the rows' image sums and mask words of this tile
+      if constexpr (decltype(first)::value && S == 0) {  // the rows' image sums and mask words of this tile
         const int64_t row = r0 + lr < a.n ? r0 + lr : a.n - 1;
         if constexpr (I8)
           rsum = *reinterpret_cast<const f32x4*>(a.rowinfo + row * kI8RowInfo);
@@ -1778,7 +1787,7 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
                                     : reinterpret_cast<const uint32_t*>(a.rowinfo) + row * (I8 ? kI8RowInfo : 1);
         mword = *mp | (masked ? 0u : ~0u);
       }
-      compute(xa[S], rslot);
+      compute(xa[S], rslot, std::bool_constant<decltype(first)::value && S == 0>{});
       rslot = rslot + 1 == kI3Slots ? 0 : rslot + 1;
       if constexpr (decltype(ld)::value) {
         load_x(xa[S], xr, xc);
@@ -1790,10 +1799,19 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
       }
     };
     using Load = std::true_type;
-    int c = 0;
-    for (; c + XS < nch; c += XS)
-      static_for<XS>([&](auto sc) { step(c, sc, Load{}); });
-    static_for<XS>([&](auto sc) { step(c, sc, std::integral_constant<bool, FX_I3_XPF>{}); });
+    using Xpf = std::integral_constant<bool, FX_I3_XPF>;
+    using First = std::true_type;
+    using Later = std::false_type;
+    // the first chunk group peeled (its first k-step starts from acc0)
+    if (nch > XS) {
+      static_for<XS>([&](auto sc) { step(0, sc, Load{}, First{}); });
+      int c = XS;
+      for (; c + XS < nch; c += XS)
+        static_for<XS>([&](auto sc) { step(c, sc, Load{}, Later{}); });
+      static_for<XS>([&](auto sc) { step(c, sc, Xpf{}, Later{}); });
+    } else {
+      static_for<XS>([&](auto sc) { step(0, sc, Xpf{}, First{}); });
+    }
     if (tid < fBM) {  // one thread per row: bound factor, flags
       // (the row index recomputed here from opaque(tid): hoisted out of the
       // tile loop, its flag bit was spilled and reloaded behind a vmcnt(0))
