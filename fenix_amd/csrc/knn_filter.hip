@@ -859,17 +859,17 @@ __device__ __forceinline__ void filter_tiles(const FilterArgs& a, unsigned char*
 // candidate buffer: one global atomic per query reserves the slots.  seg =
 // [fBQ counters][fBQ x SEG entries {lb key, ub key, row}]; called by every
 // thread after the last tile (ends with the counters reused as bases).
-template <int SEG>
+template <int SEG, int NT = fThreads>
 __device__ __forceinline__ void filter_flush_segments(uint32_t* seg, uint32_t* base,
                                                       const FilterArgs& a, int64_t q0, int tid) {
   __syncthreads();
-  for (int q = tid; q < fBQ; q += fThreads) {
+  for (int q = tid; q < fBQ; q += NT) {
     const uint32_t n = seg[q] < (uint32_t)SEG ? seg[q] : (uint32_t)SEG;
     seg[q] = n;
     base[q] = n != 0u && q0 + q < a.nq ? atomicAdd(&a.count[(q0 + q) * kCountStride], n) : 0u;
   }
   __syncthreads();
-  for (int i = tid; i < fBQ * SEG; i += fThreads) {
+  for (int i = tid; i < fBQ * SEG; i += NT) {
     const int q = i / SEG, j = i % SEG;
     if ((uint32_t)j >= seg[q]) continue;
     const uint32_t p = base[q] + (uint32_t)j;
@@ -1162,27 +1162,40 @@ static int launch_img2(const FilterArgs& a, int metric, hipStream_t stream) {
 #ifndef FX_I3_SEG
 #define FX_I3_SEG 24  // LDS append entries per query (overflow: global slots)
 #endif
+#ifndef FX_I3_BPF
+#define FX_I3_BPF 1   // B-fragment reads of a k-step ahead of its MFMAs (see compute)
+#endif
 #ifndef FX_I3_XPF
 #define FX_I3_XPF 0   // 1: the next tile's first image chunks in flight during the
                       // epilogue (equal with 4 stages, 1-2 % faster with 2)
 #endif
+#ifndef FX_I3_WAVES
+#define FX_I3_WAVES 8  // waves per workgroup: 8 (one 256-row workgroup per CU) or 4
+                       // (two independent 128-row workgroups per CU)
+#endif
+constexpr int kI3Waves = FX_I3_WAVES;
+constexpr int kI3Threads = 64 * kI3Waves;
+constexpr int kI3BM = 32 * kI3Waves;    // rows per workgroup tile (one 32-row tile per wave)
+constexpr int kI3Sub = fBM / kI3BM;     // workgroup tiles per fBM-row tile of the phase plan
 constexpr int kI3Slots = FX_I3_QA + 1;
 constexpr int kI3QBytes = fBQ * fBK * 2;               // one slot: 16 KB
-constexpr int kI3QDma = kI3QBytes / 1024 / fWaves;     // 1-KB DMAs per wave per chunk
-static_assert(kI3QDma * 1024 * fWaves == kI3QBytes && fBK == 32, "query ring");
+constexpr int kI3QDma = kI3QBytes / 1024 / kI3Waves;   // 1-KB DMAs per wave per chunk
+static_assert(kI3QDma * 1024 * kI3Waves == kI3QBytes && fBK == 32, "query ring");
+static_assert(kI3Sub * kI3BM == fBM && kI3Waves <= fWaves, "workgroup tile");
 struct Img3Shared {
   unsigned char qring[kI3Slots][kI3QBytes];
-  float rinfo[fBM];
-  float rterm[fBM];
+  float rinfo[kI3BM];
+  float rterm[kI3BM];
   uint32_t rflags[2][kRowFlagWords];
   f32x4 qtab[fBQ];
   float2 qab[fBQ];
   uint32_t seg[fBQ + 3 * fBQ * FX_I3_SEG];  // counters, then entries {lb key, ub key, row}
   uint32_t segbase[fBQ];
-  float rext[fBM];   // int8 image: 1 / s of the row
+  float rext[kI3BM];  // int8 image: 1 / s of the row
   f32x4 qinf[fBQ];   // int8 image: the query's launch_qprep8 record
 };
-static_assert(sizeof(Img3Shared) <= 160 * 1024, "filter_img3_kernel: LDS over 160 KB");
+static_assert(sizeof(Img3Shared) * (fWaves / kI3Waves) <= 160 * 1024,
+              "filter_img3_kernel: LDS over 160 KB per CU");
 
 typedef __attribute__((address_space(3))) void* i3_lds_ptr;
 
@@ -1589,7 +1602,7 @@ __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const fl
 }
 
 template <int METRIC, bool I8>
-__global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(FilterArgs a) {
+__global__ void __launch_bounds__(kI3Threads, 2) filter_img3_kernel(FilterArgs a) {
   constexpr int XS = FX_I3_XS, SEG = FX_I3_SEG;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   Img3Shared* sh = reinterpret_cast<Img3Shared*>(smem);
@@ -1610,14 +1623,19 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
   const int nch = ((a.d + CK - 1) / CK + XS - 1) / XS * XS;
   const int ksteps = I8 ? (a.d + 31) / 32 : (a.d + 15) / 16;
   const int64_t ntile32 = (a.n + 31) / 32;
-  if ((int64_t)blockIdx.x >= a.num_tiles) return;
+  // workgroup tiles: kI3Sub per fBM-row tile of the plan (a.tile_start, ...)
+  const int64_t ntiles = a.num_tiles * kI3Sub;
+  auto tile_r0 = [&](int64_t ti) {
+    return (a.tile_start + (ti / kI3Sub) * a.tile_stride) * fBM + (ti % kI3Sub) * kI3BM;
+  };
+  if ((int64_t)blockIdx.x >= ntiles) return;
   if constexpr (I8)
-    i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, fThreads);
+    i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, kI3Threads);
   else
-    filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, fThreads);
-  for (int q = tid; q < fBQ; q += fThreads) sh->seg[q] = 0u;  // (ordered by the first barrier)
+    filter_query_table<METRIC>(a, q0, sh->qtab, sh->qab, tid, kI3Threads);
+  for (int q = tid; q < fBQ; q += kI3Threads) sh->seg[q] = 0u;  // (ordered by the first barrier)
   // the ring starts zeroed (a slot whose DMA is dropped then holds finite values)
-  for (int i = tid; i < kI3Slots * kI3QBytes / 16; i += fThreads)
+  for (int i = tid; i < kI3Slots * kI3QBytes / 16; i += kI3Threads)
     reinterpret_cast<i32x4*>(sh->qring)[i] = i32x4(0);
   __syncthreads();
 
@@ -1657,8 +1675,8 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
   // this wave's 32-row tile of the row tile at step iteration ti: its
   // k-steps, one KB each (a tile past the end: an empty descriptor, zeros)
   auto x_rsrc = [&](int64_t ti) {
-    const int64_t t32 = (a.tile_start + ti * a.tile_stride) * (fBM / 32) + wid;
-    const int64_t live = (ti < a.num_tiles && t32 < ntile32) ? 1 : 0;
+    const int64_t t32 = tile_r0(ti) / 32 + wid;
+    const int64_t live = (ti < ntiles && t32 < ntile32) ? 1 : 0;
     const unsigned char* base = reinterpret_cast<const unsigned char*>(a.X) +
                                 (live ? t32 : 0) * (int64_t)ksteps * 1024;
     const uint64_t xp = reinterpret_cast<uint64_t>(base);
@@ -1709,23 +1727,60 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
       return;
     }
     const unsigned char* st = sh->qring[slot];
+    // B fragments of a k-step read into their own registers before its
+    // MFMAs (FX_I3_BPF 1; 2: both k-steps' first): left to itself, hipcc
+    // read each fragment into one register set right before its MFMA and
+    // waited lgkmcnt(0) in between, so every MFMA paid a full LDS latency
+    auto mfma = [&](int u, const f16x8& xv, const f16x8& bv, bool start) {
+      const f32x16 cin = start ? acc0 : acc[u];
+      if constexpr (I8) {
+        typedef int i32x16 __attribute__((ext_vector_type(16)));
+        acc[u] = __builtin_bit_cast(f32x16, __builtin_amdgcn_mfma_i32_32x32x32_i8(
+            __builtin_bit_cast(i32x4, xv), __builtin_bit_cast(i32x4, bv),
+            __builtin_bit_cast(i32x16, cin), 0, 0, 0));
+      } else {
+        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xv, bv, cin, 0, 0, 0);
+      }
+    };
+#if FX_I3_BPF != 0
+    // (query tile u sits 32 x 64 B further: (Q + 32 u) has the same swizzle)
+    auto read_b = [&](f16x8 (&bv)[kI2QT], int s) {
+#pragma unroll
+      for (int u = 0; u < kI2QT; ++u)
+        bv[u] = *reinterpret_cast<const f16x8*>(st + bq[s] + u * 32 * 64);
+    };
+#endif
+#if FX_I3_BPF == 0
     static_for<kI2KS>([&](auto sc) {
       constexpr int s = decltype(sc)::value;
 #pragma unroll
       for (int u = 0; u < kI2QT; ++u) {
-        // (query tile u sits 32 x 64 B further: (Q + 32 u) has the same swizzle)
         const f16x8 bv = *reinterpret_cast<const f16x8*>(st + bq[s] + u * 32 * 64);
-        const f32x16 cin = (FIRST && s == 0) ? acc0 : acc[u];
-        if constexpr (I8) {
-          typedef int i32x16 __attribute__((ext_vector_type(16)));
-          acc[u] = __builtin_bit_cast(f32x16, __builtin_amdgcn_mfma_i32_32x32x32_i8(
-              __builtin_bit_cast(i32x4, xa[s]), __builtin_bit_cast(i32x4, bv),
-              __builtin_bit_cast(i32x16, cin), 0, 0, 0));
-        } else {
-          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bv, cin, 0, 0, 0);
-        }
+        mfma(u, xa[s], bv, FIRST && s == 0);
       }
     });
+#elif FX_I3_BPF == 1
+    static_for<kI2KS>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      f16x8 bv[kI2QT];
+      read_b(bv, s);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < kI2QT; ++u) mfma(u, xa[s], bv[u], FIRST && s == 0);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+#else
+    static_assert(kI2KS == 2, "FX_I3_BPF 2: two k-steps per chunk");
+    f16x8 b0[kI2QT], b1[kI2QT];
+    read_b(b0, 0);
+    read_b(b1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kI2QT; ++u) mfma(u, xa[0], b0[u], FIRST);
+#pragma unroll
+    for (int u = 0; u < kI2QT; ++u) mfma(u, xa[1], b1[u], false);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
   };
 
   // ---- prologue: query chunks 0 .. QA-1 and image chunks 0 .. XS-1 of the
@@ -1752,9 +1807,9 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (once: the prologue's order differs)
   int rslot = 0;  // slot of the query chunk the next step reads
   int par = 0;
-  const int lr = tid & (fBM - 1);  // the row this thread notes (threads >= fBM: duplicates)
-  for (int64_t ti = blockIdx.x; ti < a.num_tiles; ti += gridDim.x, par ^= 1) {
-    const int64_t r0 = (a.tile_start + ti * a.tile_stride) * fBM;
+  const int lr = tid & (kI3BM - 1);  // the row this thread notes (threads >= kI3BM: duplicates)
+  for (int64_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x, par ^= 1) {
+    const int64_t r0 = tile_r0(ti);
     if (tid < kRowFlagWords) sh->rflags[par][tid] = 0u;  // (read two tiles back)
     std::conditional_t<I8, f32x4, float> rsum = {};
     uint32_t mword = 0u;
@@ -1763,13 +1818,19 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
     // the end of a tile, FX_I3_XPF)
     auto step = [&](int c, auto sc, auto ld, auto first) {
       constexpr int S = decltype(sc)::value;
-      // query chunk c + S landed (this wave's DMAs; the loads issued after
-      // it: the image chunk of its step, then QA - 1 steps of both), and
-      // every wave done with the slot refilled next
+      // query chunk c + S landed (this wave's DMAs; vmcnt retires in issue
+      // order, and the loads issued after it are QA - 1 steps' DMAs plus the
+      // image chunks of the QA steps from its own: none in a group that loads
+      // nothing, i.e. the tile's last group without FX_I3_XPF, where only the
+      // steps before the group's start loaded; extra loads, e.g. the rows'
+      // terms, only make the wait stronger), and every wave done with the
+      // slot refilled next
+      constexpr bool LD = decltype(ld)::value;
+      constexpr int kXAfter = LD ? FX_I3_QA : (FX_I3_QA > S ? FX_I3_QA - S : 0);
       if (diag & 16)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else
-        i3_wait_barrier<kI2KS + (FX_I3_QA - 1) * (kI3QDma + kI2KS)>();
+        i3_wait_barrier<(FX_I3_QA - 1) * kI3QDma + kXAfter * kI2KS>();
       issue_q(qc, qslot);
       qc = qc + 1 == nch ? 0 : qc + 1;
       qslot = qslot + 1 == kI3Slots ? 0 : qslot + 1;
@@ -1812,7 +1873,7 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
     } else {
       static_for<XS>([&](auto sc) { step(0, sc, Xpf{}, First{}); });
     }
-    if (tid < fBM) {  // one thread per row: bound factor, flags
+    if (tid < kI3BM) {  // one thread per row: bound factor, flags
       // (the row index recomputed here from opaque(tid): hoisted out of the
       // tile loop, its flag bit was spilled and reloaded behind a vmcnt(0))
       const int lr = (int)opaque((unsigned)tid);
@@ -1860,7 +1921,7 @@ __global__ void __launch_bounds__(fThreads, fWaves / 4) filter_img3_kernel(Filte
   // the ring's and the stream's last loads (past the end) land before the
   // workgroup's LDS is released; then the segments go out
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  filter_flush_segments<SEG>(sh->seg, sh->segbase, a, q0, tid);
+  filter_flush_segments<SEG, kI3Threads>(sh->seg, sh->segbase, a, q0, tid);
 }
 
 static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
@@ -1877,8 +1938,8 @@ static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
   int rc = device_cus(&cus);
   if (rc) return rc;
   const int64_t qtiles = (a.nq + fBQ - 1) / fBQ;
-  int64_t bx = cus;
-  if (bx > a.num_tiles) bx = a.num_tiles;
+  int64_t bx = (int64_t)cus * (fWaves / kI3Waves);  // one or two workgroups per CU
+  if (bx > a.num_tiles * kI3Sub) bx = a.num_tiles * kI3Sub;
   for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
     FilterArgs b = a;
     const int64_t yn = (qtiles - y0) < 65535 ? (qtiles - y0) : 65535;
@@ -1890,7 +1951,7 @@ static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
     if (a.cand_ub) b.cand_ub = a.cand_ub + y0 * fBQ * (int64_t)a.cap;
     b.nq = a.nq - y0 * fBQ;
     void* args[] = {(void*)&b};
-    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(fThreads), args,
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(kI3Threads), args,
                                    smem, stream);
     if (e != hipSuccess) {
       set_error("filter_img3_kernel launch: %s", hipGetErrorString(e));
