@@ -2,10 +2,14 @@
 
 Workload (BASELINE.json configs[1], the headline metric's config): one query,
 10M x 768 float32 rows per GPU, L2, k=100, corpus resident in HBM.  One
-"step" = one exact search = fused scan + top-k over every row of this rank's
-shard, merge to the final sorted k, and for N > 1 the RCCL all-gather of the
-per-rank top-k plus the final merge (weak scaling: 10M rows per GPU, so N=8 is
-configs[3], 80M rows).
+"step" = one exact search over every row of this rank's shard, merge to the
+final sorted k, and for N > 1 the RCCL all-gather of the per-rank top-k plus
+the final merge (weak scaling: 10M rows per GPU, so N=8 is configs[3], 80M
+rows).  The search is the product default: for a >= 4 GiB f32 shard it
+streams the resident int8 filter image (built once per corpus version, timed
+apart as filter_image.build_ms) through the int8-MFMA bound filter and
+rescores the candidates from the f32 rows, bit-identical to the exact fused
+scan, which the record times beside it (exact_scan).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rows ROWS] [--d D]
                     [--k K] [--nq Q] [--metric l2|cosine|inner_product]
@@ -298,21 +302,42 @@ def main():
     scan_bytes = n * d * esize + nq * d * 4
     tag = f"{n}x{d}_{args.dtype}_{args.metric}_k{k}_q{nq}"
     traffic = pmc_traffic(tag, _lib.library_sha())
-    # batched queries: the fp16-MFMA bound filter + exact rescoring
+    # batched queries: the MFMA bound filter + exact rescoring
     # (knn_filter.hip), one HBM-bound pass over the corpus (capi.hip
     # use_batched: from "batch_min_queries" queries, f32 rows with d % 4 == 0,
-    # f16 rows with d % 8 == 0)
+    # f16 rows with d % 8 == 0; a single query over a >= 4 GiB f32 corpus
+    # when the engine supplies an int8 filter image, which it builds exactly
+    # when the library will read it: fx_filter_image_used)
     min_q = max(1, _lib.get_option("batch_min_queries"))
     batched = (_lib.get_option("batched") != 0 and nq >= min_q and not qu8
                and ((args.dtype == "f32" and d % 4 == 0) or (args.dtype == "f16" and d % 8 == 0)))
-    filt = batched
-    image = eng._images.get(id(x)) if filt and args.dtype == "f32" else None
+    image = eng._images.get(id(x)) if args.dtype == "f32" and not qu8 else None
+    filt = batched or image is not None
     bits = image[0][3] if image is not None else 16
     if image is not None:
         # the phases stream the filter image and its row terms instead of the
         # f32 rows: those are the bytes of the pass (the rescoring reads a
         # few thousand f32 rows per query on top)
         scan_bytes = n * d * bits // 8 + n * (16 if bits == 8 else 4) + nq * d * 4
+    # the exact f32 scan of the same search beside it (single queries through
+    # the filter image only): option single_query_image=0, same steps
+    exact_scan = None
+    if image is not None and nq == 1:
+        with _lib.options(single_query_image=0):
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            xs_ms = (time.perf_counter() - t1) * 1e3 / args.steps
+        xs_bytes = n * d * esize + nq * d * 4
+        exact_scan = {"ms_per_step": xs_ms, "vectors_per_s": n * world * nq / (xs_ms * 1e-3),
+                      "hbm_frac": xs_bytes / (xs_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                      "note": "the exact fused f32 scan + merge of the same query "
+                              "(option single_query_image=0), the path of rounds 1-2"}
+
     achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
     if filt:
         kname = (f"fx::filter_img3_kernel ({'int8' if bits == 8 else 'fp16'}-MFMA bound filter, "
@@ -384,6 +409,7 @@ def main():
                                          "fp16 or none"}}
                if image is not None else {}),
             "roofline": roof,
+            **({"exact_scan": exact_scan} if exact_scan is not None else {}),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

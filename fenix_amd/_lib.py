@@ -56,6 +56,7 @@ SYMBOLS = (
     "fx_filter_image8",
     "fx_knn_scan_img8",
     "fx_knn_search_img8",
+    "fx_knn_reduce_img8",
     "fx_knn_distances",
     "fx_topk_merge_workspace_bytes",
     "fx_topk_merge",
@@ -87,7 +88,7 @@ SYMBOLS = (
 # "batched", "batch_min_queries" and "filter_image" are user switches, the rest
 # test switches
 OPTIONS = ("batched", "batch_min_queries", "batch_cap", "batch_sample_ratio", "force_fallback",
-           "scan_interleave", "q8_dma", "filter_image", "batch_ub_test")
+           "scan_interleave", "q8_dma", "filter_image", "batch_ub_test", "single_query_image")
 
 _lock = threading.Lock()
 _lib = None
@@ -162,6 +163,9 @@ def load() -> ctypes.CDLL:
         L.fx_knn_scan_img8.restype = ci
         L.fx_knn_search_img8.argtypes = L.fx_knn_search_img.argtypes
         L.fx_knn_search_img8.restype = ci
+        L.fx_knn_reduce_img8.argtypes = [vp, ci, i64, i64, i64, vp, vp, i64, ci, i64, vp, vp, sz,
+                                         vp, vp, vp]
+        L.fx_knn_reduce_img8.restype = ci
         L.fx_knn_distances.argtypes = [vp, ci, i64, i64, vp, i64, ci, vp, vp, vp]
         L.fx_knn_distances.restype = ci
         L.fx_topk_merge_workspace_bytes.argtypes = [i64, i64, i64, i64, ctypes.POINTER(sz)]

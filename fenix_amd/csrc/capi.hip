@@ -40,8 +40,9 @@ static std::mutex g_mu;
 // ----------------------------------------------------------------- options --
 static const char* const kOptNames[kOptCount] = {
     "batched", "batch_min_queries", "batch_cap", "batch_sample_ratio",
-    "force_fallback", "scan_interleave", "q8_dma", "filter_image", "batch_ub_test"};
-static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}, {8}, {1}};
+    "force_fallback", "scan_interleave", "q8_dma", "filter_image", "batch_ub_test",
+    "single_query_image"};
+static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}, {8}, {1}, {1}};
 
 int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
 
@@ -207,12 +208,21 @@ struct BatchLayout {
 // rejected fp32-MFMA batch kernel (knn_batch.hip) behind FX_BATCH_FILTER=0.
 static bool use_filter() { return diag_env("FX_BATCH_FILTER", 1) != 0; }
 
-static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool aligned) {
+// A single query over an f32 corpus of at least this many bytes takes the
+// batched path when an int8 filter image is supplied (the *_img8 entry
+// points, option "single_query_image"): 10M x 768 1.41 vs 4.34 ms; the
+// filter path's fixed cost (~0.25 ms of small launches) loses below ~2.4 GB
+static constexpr int64_t kSingleImageMinBytes = (int64_t)4 << 30;
+
+static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool aligned, int64_t n,
+                        bool img8) {
   if (option(kOptBatched) == 0) return false;
   // 2 queries: 6.5 ms vs 2 x 4.5 ms (10Mx768); "batch_min_queries" = 1 also
-  // sends single queries through the filter (with a filter image that halves
-  // their bytes; the default keeps the exact scan)
+  // sends every single query through the filter
   int64_t min_q = option(kOptBatchMinQ) >= 1 ? option(kOptBatchMinQ) : 2;
+  if (nq == 1 && img8 && option(kOptSingleImage) != 0 && dtype == FX_DTYPE_F32 && d % 8 == 0 &&
+      n * d * 4 >= kSingleImageMinBytes)
+    min_q = 1;
   if (!use_filter()) min_q = 8;  // the fp32-MFMA kernel breaks even with scans at ~8 queries
   if (nq < min_q || !aligned) return false;
   // the rescoring repeats the scan's 16-B slot order: f32 rows need d % 4 == 0,
@@ -365,10 +375,12 @@ static int plan_fallback(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k,
   return FX_OK;
 }
 
+// img8: the call supplies an int8 filter image (single queries may take
+// the batched path, use_batched); the reduce must plan with the same flag
 static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
-                       bool aligned, SearchLayout* s) {
+                       bool aligned, SearchLayout* s, bool img8 = false) {
   if (k > kMaxK) return plan_large_search(n, d, dtype, nq, metric, aligned, s);
-  if (!use_batched(nq, dtype, metric, d, aligned)) {
+  if (!use_batched(nq, dtype, metric, d, aligned, n, img8)) {
     return plan_single(n, d, dtype, nq, k, metric, aligned, s);
   }
   // the single-query plan over fb_queries queries serves overflowing queries
@@ -646,10 +658,12 @@ int fx_knn_workspace_bytes(int64_t n, int64_t d, int dtype, int64_t nq, int64_t 
   size_t best = 0;
   for (int metric = 0; metric < 3; ++metric) {
     for (int aligned = 0; aligned < 2; ++aligned) {
-      SearchLayout s;
-      rc = plan_search(n, d, dtype, nq, k, metric, aligned != 0, &s);
-      if (rc) return rc;
-      if (s.total > best) best = s.total;
+      for (int img8 = 0; img8 < 2; ++img8) {
+        SearchLayout s;
+        rc = plan_search(n, d, dtype, nq, k, metric, aligned != 0, &s, img8 != 0);
+        if (rc) return rc;
+        if (s.total > best) best = s.total;
+      }
     }
   }
   *out_bytes = best;
@@ -657,7 +671,8 @@ int fx_knn_workspace_bytes(int64_t n, int64_t d, int dtype, int64_t nq, int64_t 
 }
 
 static int search_layout(const void* corpus, int dtype, int64_t n, int64_t d, int64_t nq,
-                         int metric, int64_t k, void* ws, size_t ws_bytes, SearchLayout* s) {
+                         int metric, int64_t k, void* ws, size_t ws_bytes, SearchLayout* s,
+                         bool img8 = false) {
   int rc = validate(n, d, dtype, nq, metric);
   if (rc) return rc;
   if (k < 1 || k > kLargeMaxK) {
@@ -669,7 +684,7 @@ static int search_layout(const void* corpus, int dtype, int64_t n, int64_t d, in
     return FX_EINVAL;
   }
   const bool aligned = ((uintptr_t)corpus % 16) == 0;
-  rc = plan_search(n, d, dtype, nq, k, metric, aligned, s);
+  rc = plan_search(n, d, dtype, nq, k, metric, aligned, s, img8);
   if (rc) return rc;
   if (ws_bytes < s->total) {
     set_error("workspace too small: %zu < %zu", ws_bytes, s->total);
@@ -691,7 +706,8 @@ static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_
                      int64_t nq, int metric, int64_t k, const uint32_t* mask, void* ws,
                      size_t ws_bytes, void* stream) {
   SearchLayout s;
-  int rc = search_layout(corpus, dtype, n, d, nq, metric, k, ws, ws_bytes, &s);
+  int rc = search_layout(corpus, dtype, n, d, nq, metric, k, ws, ws_bytes, &s,
+                         img8 && image != nullptr);
   if (rc) return rc;
   if (!queries) {
     set_error("null pointer argument");
@@ -875,18 +891,20 @@ int fx_filter_image_used(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k,
     return FX_EUNSUPPORTED;
   }
   SearchLayout s;
-  rc = plan_search(n, d, dtype, nq, k, metric, true, &s);
+  // (the int8 image, the host's default, also serves single queries over
+  // large corpora: use_batched)
+  rc = plan_search(n, d, dtype, nq, k, metric, true, &s, option(kOptFilterImage) == 8);
   if (rc) return rc;
   *out = image_applies(s, dtype, d) ? 1 : 0;
   return FX_OK;
 }
 
-int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
-                  const float* queries, int64_t nq, int metric, int64_t k,
-                  const uint32_t* mask, void* ws, size_t ws_bytes, float* out_dist,
-                  int64_t* out_row, void* stream) {
+static int reduce_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                       const float* queries, int64_t nq, int metric, int64_t k,
+                       const uint32_t* mask, void* ws, size_t ws_bytes, float* out_dist,
+                       int64_t* out_row, void* stream, bool img8) {
   SearchLayout s;
-  int rc = search_layout(corpus, dtype, n, d, nq, metric, k, ws, ws_bytes, &s);
+  int rc = search_layout(corpus, dtype, n, d, nq, metric, k, ws, ws_bytes, &s, img8);
   if (rc) return rc;
   if (!out_dist || !out_row) {
     set_error("null pointer argument");
@@ -915,6 +933,22 @@ int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t r
   return fallback_search(s, corpus, dtype, n, d, row_base, queries, nq, metric, k, mask,
                          reinterpret_cast<const uint32_t*>(w + b.off_count), gate_cap,
                          w + s.single_off, out_dist, out_row, st);
+}
+
+int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                  const float* queries, int64_t nq, int metric, int64_t k,
+                  const uint32_t* mask, void* ws, size_t ws_bytes, float* out_dist,
+                  int64_t* out_row, void* stream) {
+  return reduce_impl(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
+                     out_dist, out_row, stream, false);
+}
+
+int fx_knn_reduce_img8(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
+                       const void* image, const float* queries, int64_t nq, int metric, int64_t k,
+                       const uint32_t* mask, void* ws, size_t ws_bytes, float* out_dist,
+                       int64_t* out_row, void* stream) {
+  return reduce_impl(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
+                     out_dist, out_row, stream, image != nullptr);
 }
 
 int fx_knn_search(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
@@ -958,8 +992,8 @@ int fx_knn_search_img8(const void* corpus, int dtype, int64_t n, int64_t d, int6
   int rc = fx_knn_scan_img8(corpus, dtype, n, d, row_base, image, rowinfo, queries, nq, metric, k,
                             mask, ws, ws_bytes, stream);
   if (rc) return rc;
-  return fx_knn_reduce(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
-                       out_dist, out_row, stream);
+  return reduce_impl(corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, ws, ws_bytes,
+                     out_dist, out_row, stream, image != nullptr);
 }
 
 int fx_knn_search_rows_workspace_bytes(int64_t nrows, int64_t d, int dtype, int64_t nq,

@@ -23,6 +23,7 @@ enum Option : int {
   kOptQ8Dma,
   kOptFilterImage,  // filter image bits for f32 corpora (engine policy): 8, 16 or 0 (none)
   kOptBatchUbTest,  // sampling phases append by upper bound (0: by lower bound, test switch)
+  kOptSingleImage,  // single queries over large f32 corpora through a supplied int8 image
   kOptCount
 };
 int64_t option(Option o);

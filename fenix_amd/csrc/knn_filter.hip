@@ -89,7 +89,7 @@ namespace FX_FILTER_IMPL {
 #endif
 #ifndef FX_FILTER_IMG3  // the 256-query, 32-wide-K build (knn_filter.hip itself):
                         // filter_img3_kernel serves tiled filter images
-#if FX_FILTER_BQ == 256 && FX_FILTER_BK == 32
+#if FX_FILTER_BK == 32 && FX_FILTER_BQ >= 128
 #define FX_FILTER_IMG3 1
 #else
 #define FX_FILTER_IMG3 0
@@ -114,7 +114,9 @@ constexpr int fStages = FX_FILTER_STAGES;
 constexpr bool kXpf = FX_FILTER_XPF;
 static_assert(fStages == 2, "the K loop alternates two register stages and two LDS buffers");
 constexpr int fQC = fBK / 8;                    // 16-B f16 pieces per query per chunk
-constexpr int fQP = fBQ * fQC / fThreads;       // Q pieces per thread per chunk
+// Q pieces per thread per chunk (a build with no register-staged kernels,
+// FX_FILTER_ROWS 0, may have fewer pieces than threads)
+constexpr int fQP = fBQ * fQC / fThreads > 0 ? fBQ * fQC / fThreads : 1;
 // Rows of type XT (float or _Float16) come in 16-B pieces of E elements;
 // C pieces per row per chunk (the lanes sharing a row), P per thread.
 template <typename XT>
@@ -125,7 +127,7 @@ struct XPiece {
   static_assert(P >= 1 && fThreads % C == 0, "row staging");
 };
 static_assert(fQG >= 1 && fRG * fQG == fWaves && fQT >= 1, "wave grid");
-static_assert(fQP >= 1 && fBK % 16 == 0, "staging");
+static_assert((FX_FILTER_ROWS == 0 || fBQ * fQC / fThreads >= 1) && fBK % 16 == 0, "staging");
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -1177,10 +1179,18 @@ constexpr int kI3Waves = FX_I3_WAVES;
 constexpr int kI3Threads = 64 * kI3Waves;
 constexpr int kI3BM = 32 * kI3Waves;    // rows per workgroup tile (one 32-row tile per wave)
 constexpr int kI3Sub = fBM / kI3BM;     // workgroup tiles per fBM-row tile of the phase plan
+#ifndef FX_I3_BPC
+#define FX_I3_BPC (fWaves / FX_I3_WAVES)  // workgroups per CU in the launch
+#endif
 constexpr int kI3Slots = FX_I3_QA + 1;
-constexpr int kI3QBytes = fBQ * fBK * 2;               // one slot: 16 KB
-constexpr int kI3QDma = kI3QBytes / 1024 / kI3Waves;   // 1-KB DMAs per wave per chunk
-static_assert(kI3QDma * 1024 * kI3Waves == kI3QBytes && fBK == 32, "query ring");
+constexpr int kI3QBytes = fBQ * fBK * 2;               // one slot: 16 KB (256 queries)
+constexpr int kI3QDmaAll = kI3QBytes / 1024;           // 1-KB DMAs per chunk
+// 1-KB DMAs per wave per chunk: every wave the same count, or (64-query tiles:
+// 4 KB per chunk) one each on the first kI3QDmaAll waves and none on the rest
+constexpr int kI3QDma = kI3QDmaAll >= kI3Waves ? kI3QDmaAll / kI3Waves : 1;
+static_assert((kI3QDmaAll >= kI3Waves ? kI3QDma * kI3Waves : kI3QDmaAll) == kI3QDmaAll &&
+                  kI3QDmaAll * 1024 == kI3QBytes && fBK == 32,
+              "query ring");
 static_assert(kI3Sub * kI3BM == fBM && kI3Waves <= fWaves, "workgroup tile");
 struct Img3Shared {
   unsigned char qring[kI3Slots][kI3QBytes];
@@ -1665,6 +1675,7 @@ __global__ void __launch_bounds__(kI3Threads, 2) filter_img3_kernel(FilterArgs a
   const int qchunks = a.dq / CK;
   auto issue_q = [&](int c, int slot) {
     if (diag & 8) return;
+    if (kI3QDmaAll < kI3Waves && wid >= kI3QDmaAll) return;  // (wave-uniform)
     unsigned char* st = sh->qring[slot];
 #pragma unroll
     for (int i = 0; i < kI3QDma; ++i)
@@ -1938,7 +1949,7 @@ static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
   int rc = device_cus(&cus);
   if (rc) return rc;
   const int64_t qtiles = (a.nq + fBQ - 1) / fBQ;
-  int64_t bx = (int64_t)cus * (fWaves / kI3Waves);  // one or two workgroups per CU
+  int64_t bx = (int64_t)cus * FX_I3_BPC;  // workgroups per CU
   if (bx > a.num_tiles * kI3Sub) bx = a.num_tiles * kI3Sub;
   for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
     FilterArgs b = a;
@@ -3217,6 +3228,9 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_
 namespace q128 {
 int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_q128.hip
 }
+namespace q64i {
+int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_q64i.hip
+}
 namespace h256 {
 int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_h256.hip
 }
@@ -3234,8 +3248,12 @@ bool filter_ring() { return diag_env("FX_FILTER_RING", 0) != 0; }
 // Batches of <= 64 queries take the 64-query tiles, 65..128 the 128-query ones
 // (their Qh is padded to 64 / 128, filter_query_pad)
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
-  // int8 images: the 256-query kernel for every batch (its queries padded to 256)
-  if (a.img8) return q256::launch(a, metric, stream);
+  // int8 images: filter_img3_kernel with 64-, 128- or 256-query tiles
+  if (a.img8) {
+    if (a.nq <= 64) return q64i::launch(a, metric, stream);
+    if (a.nq <= 128) return q128::launch(a, metric, stream);
+    return q256::launch(a, metric, stream);
+  }
   if (a.nq <= 64) return q64::launch(a, metric, stream);
   if (a.nq <= 128 && !filter_ring()) return q128::launch(a, metric, stream);
   // tiled images: K chunks of 32 (5.07-5.10 vs 5.48-5.49 ms for configs[2]

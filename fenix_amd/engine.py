@@ -556,11 +556,23 @@ class Engine:
     def reduce(self, shard: Shard, queries: torch.Tensor, metric: int, k: int, ws: torch.Tensor,
                out_dist: torch.Tensor, out_row: torch.Tensor,
                mask: Optional[torch.Tensor] = None) -> None:
-        """Phase 2 of search_shard (fx_knn_reduce), same arguments as scan."""
+        """Phase 2 of search_shard (fx_knn_reduce), same arguments as scan.  A
+        scan that received an int8 filter image is completed by
+        fx_knn_reduce_img8 with the same image (the library may have planned a
+        single query through the filter)."""
+        nq = queries.shape[0]
+        img, _, bits = self.filter_image(shard, nq, k, metric)
+        L = _lib.load()
+        if bits == 8 and img is not None:
+            _lib.check(L.fx_knn_reduce_img8(
+                _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base, _ptr(img),
+                _ptr(queries), nq, metric, k, _ptr(mask), _ptr(ws), ws.numel(),
+                _ptr(out_dist), _ptr(out_row), self._stream()))
+            return
         _lib.check(
-            _lib.load().fx_knn_reduce(
+            L.fx_knn_reduce(
                 _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base,
-                _ptr(queries), queries.shape[0], metric, k, _ptr(mask), _ptr(ws), ws.numel(),
+                _ptr(queries), nq, metric, k, _ptr(mask), _ptr(ws), ws.numel(),
                 _ptr(out_dist), _ptr(out_row), self._stream(),
             )
         )
