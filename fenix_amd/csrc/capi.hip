@@ -477,10 +477,13 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
     if (rc) return rc;
   }
   hipError_t e = hipMemsetAsync(thr, 0xFF, (size_t)nq * 8, st);
+  // a one-level threshold merge resets the counts it read, so only the first
+  // phase needs a fill (each fill is a ~5 us launch)
+  const bool merge_zeroes = b.merge.levels == 1;
   for (int ph = 0; ph < b.nphases && e == hipSuccess; ++ph) {
     const bool last = ph + 1 == b.nphases;
     // (the lists are read up to count only: no fill of the candidate buffers)
-    e = hipMemsetAsync(count, 0, (size_t)nq * 4 * kCountStride, st);
+    if (ph == 0 || !merge_zeroes) e = hipMemsetAsync(count, 0, (size_t)nq * 4 * kCountStride, st);
     if (e != hipSuccess) break;
     FilterArgs a = {};
     a.X = image != nullptr ? image : X;
@@ -520,7 +523,7 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
       float* topd = reinterpret_cast<float*>(w + b.off_topd);
       int64_t* topr = reinterpret_cast<int64_t*>(w + b.off_topr);
       rc = run_merge(b.merge, last ? cand_ub : cand, nq, k, w + b.off_merge, topd, topr, st,
-                     nullptr, nullptr, 0, count);
+                     nullptr, nullptr, 0, count, !last);
       if (rc) return rc;
       rc = launch_exact_kth(X, dtype, n, (int)d, row_base, Q, qnorm, nq, (int)k, topr, metric,
                             thr, st);
@@ -529,7 +532,7 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
     }
     // the k-th upper bound of this phase's candidates: next threshold
     rc = run_merge(b.merge, last ? cand_ub : cand, nq, k, w + b.off_merge, nullptr, nullptr, st,
-                   thr, nullptr, 0, count);
+                   thr, nullptr, 0, count, !last);
     if (rc) return rc;
   }
   if (e != hipSuccess) {
@@ -923,9 +926,9 @@ static int reduce_impl(const void* corpus, int dtype, int64_t n, int64_t d, int6
   const BatchLayout& b = s.batch;
   char* w = reinterpret_cast<char*>(ws);
   const uint64_t* cand = reinterpret_cast<const uint64_t*>(w + b.off_cand);
-  const uint32_t* count = reinterpret_cast<const uint32_t*>(w + b.off_count);
+  uint32_t* count = reinterpret_cast<uint32_t*>(w + b.off_count);
   rc = run_merge(b.merge, cand, nq, k, w + b.off_merge, out_dist, out_row, st, nullptr, nullptr,
-                 0, count);
+                 0, count);  // (the fallback gate reads the counts next: kept)
   if (rc) return rc;
   // queries whose candidates overflowed `cap`: recomputed exactly, gated on
   // the device ("force_fallback" (test switch): every query)

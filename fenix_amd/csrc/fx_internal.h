@@ -97,10 +97,12 @@ int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p)
 // gate/gate_cap: as ScanArgs::gate, per query of the merge.
 // count (optional): appended lists, query q's entries are its first
 // count[q * kCountStride] slots (capped at nlists * kin; the rest unread).
+// zero_count: reset each query's count once read (only a one-level plan,
+// where one workgroup per query reads it; ignored otherwise).
 int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, void* ws,
               float* out_dist, int64_t* out_row, hipStream_t stream,
               uint64_t* out_kth = nullptr, const uint32_t* gate = nullptr,
-              int64_t gate_cap = 0, const uint32_t* count = nullptr);
+              int64_t gate_cap = 0, uint32_t* count = nullptr, bool zero_count = false);
 
 // Batched queries (knn_batch.hip): fp32 MFMA GEMM + threshold filter.
 struct BatchArgs {

@@ -33,7 +33,7 @@ __global__ void __launch_bounds__(kMergeThreads)
                  int P2, uint64_t* __restrict__ out_lists, float* __restrict__ out_dist,
                  int64_t* __restrict__ out_row, uint64_t* __restrict__ out_kth,
                  int final_level, const uint32_t* __restrict__ gate, int64_t gate_cap,
-                 const uint32_t* __restrict__ count) {
+                 uint32_t* __restrict__ count, int zero_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   MergeShared* ms = reinterpret_cast<MergeShared*>(smem);
   uint64_t* res = reinterpret_cast<uint64_t*>(smem + sizeof(MergeShared));
@@ -56,6 +56,8 @@ __global__ void __launch_bounds__(kMergeThreads)
   const uint64_t* src = in + ((size_t)q * nlists + l0) * (size_t)kin;
   block_reset(ms);
   __syncthreads();
+  // (every thread has read count: the next phase's appends may start from 0)
+  if (zero_count && tid == 0) count[(size_t)q * kCountStride] = 0u;
   uint64_t v_or = 0, v_and = ~0ull;
   // 8 loads in flight per thread: one dependent load per iteration made every
   // level latency-bound (~50 us for 8 K entries).
@@ -188,7 +190,8 @@ int plan_merge(int64_t nq, int64_t nlists, int64_t kin, int64_t k, MergePlan* p)
 
 int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, void* ws,
               float* out_dist, int64_t* out_row, hipStream_t stream, uint64_t* out_kth,
-              const uint32_t* gate, int64_t gate_cap, const uint32_t* count) {
+              const uint32_t* gate, int64_t gate_cap, uint32_t* count, bool zero_count) {
+  const int zc = zero_count && count != nullptr && p.levels == 1 ? 1 : 0;
   const int P2 = next_pow2((int)k);
   uint64_t* bufs[2] = {reinterpret_cast<uint64_t*>(ws),
                        reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + p.ws_bytes / 2)};
@@ -212,11 +215,10 @@ int run_merge(const MergePlan& p, const uint64_t* in, int64_t nq, int64_t k, voi
       int64_t* orow = out_row ? out_row + (size_t)q0 * k : nullptr;
       uint64_t* okth = out_kth ? out_kth + q0 : nullptr;
       const uint32_t* gq = gate ? gate + (size_t)q0 * kCountStride : nullptr;
-      const uint32_t* cq = count != nullptr && lv == 0 ? count + (size_t)q0 * kCountStride
-                                                       : nullptr;
+      uint32_t* cq = count != nullptr && lv == 0 ? count + (size_t)q0 * kCountStride : nullptr;
       hipLaunchKernelGGL(merge_kernel, grid, dim3(kMergeThreads), smem, stream, src, lists,
                          (int)klen, G, (int)k, P2, dq, od, orow, okth, fin ? 1 : 0, gq, gate_cap,
-                         cq);
+                         cq, zc);
       int rc = check_launch("merge_kernel");
       if (rc) return rc;
     }
