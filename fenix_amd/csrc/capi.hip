@@ -354,13 +354,19 @@ static constexpr size_t kFallbackListBytes = (size_t)256 << 20;
 // LDS while it starts and exits (256 blocks x 256 queries of 10M x 768: 99 us
 // with nothing to do; 16 per query: a few us, and an overflowing query still
 // streams its rows from 16 CUs).
+// Small batches spread the same total over more workgroups per query (4 096
+// workgroups in all, at least 16 per query): a single query that overflows is
+// rescanned at the full scan's width (256 workgroups, ~4.4 ms for 10M x 768)
+// instead of by 16 CUs (~38 ms).
 static constexpr int64_t kFallbackBlocks = 16;
+static constexpr int64_t kFallbackTotalBlocks = 4096;
 
 static int plan_fallback(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
                          bool aligned, SearchLayout* s, int64_t* fq) {
   int rc = plan_scan(n, d, dtype, k, metric, aligned, &s->scan);
   if (rc) return rc;
-  limit_scan_blocks(&s->scan, n, kFallbackBlocks);
+  const int64_t per_q = kFallbackTotalBlocks / (nq > 0 ? nq : 1);
+  limit_scan_blocks(&s->scan, n, per_q > kFallbackBlocks ? per_q : kFallbackBlocks);
   const size_t per_query = (size_t)s->scan.nlists * k * 8;
   int64_t f = (int64_t)(kFallbackListBytes / (per_query > 0 ? per_query : 1));
   if (f > nq) f = nq;

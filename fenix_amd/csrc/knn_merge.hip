@@ -81,6 +81,29 @@ __global__ void __launch_bounds__(kMergeThreads)
   block_or_and(v_or, v_and, ms);
   __syncthreads();
 
+  // a threshold only (the batched filter's sampling phases): the k-th
+  // smallest composite is the select's threshold, no keep / sort needed
+  if (final_level && out_kth != nullptr && out_dist == nullptr && gridDim.x == 1) {
+    uint64_t kth = kEmpty;  // fewer than k entries: no threshold
+    if (m > k) {
+      const uint64_t diff = ms->all_or ^ ms->all_and;
+      const int start_shift = diff ? (63 - __clzll((long long)diff)) / 8 * 8 : 0;
+      int quota;
+      kth = block_select<kMergeThreads>(s, m, k, start_shift, ms->all_and, ms, &quota);
+    } else if (m == k) {  // exactly k entries: the k-th smallest is the largest
+      uint64_t mx = 0ull;
+      for (int i = tid; i < m; i += kMergeThreads) mx = s[i] > mx ? s[i] : mx;
+      mx = wave_max_u64(mx);
+      if (tid == 0) ms->shmax = 0ull;
+      __syncthreads();
+      if ((tid & 63) == 0) atomicMax(&ms->shmax, (unsigned long long)mx);
+      __syncthreads();
+      kth = ms->shmax;
+    }
+    if (tid == 0 && kth < out_kth[q]) out_kth[q] = kth;
+    return;
+  }
+
   int nres;
   if (m > k) {
     block_keep_k<kMergeThreads>(s, m, k, res, ms);

@@ -759,8 +759,11 @@ def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k, bits)
 @pytest.mark.parametrize("metric", METRICS)
 def test_single_query_through_filter_image(eng, monkeypatch, metric, bits):
     """"batch_min_queries" = 1: single queries take the batched filter over
-    the image (fp16: 64-query tiles, int8: 256-query tiles, one live query)
-    and still equal the scan bit for bit."""
+    the image (64-query tiles, one live query) and still equal the scan bit
+    for bit, also through the overflow fallback ("force_fallback": the
+    single query rescanned at the full scan's width).  By default a single
+    query takes the int8 image only over a >= 4 GiB f32 corpus
+    ("single_query_image")."""
     n, d, k = 80_000, 256, 100
     xh = _extreme_rows(n, d, 45)
     x = torch.from_numpy(xh).to(eng.device)
@@ -775,7 +778,19 @@ def test_single_query_through_filter_image(eng, monkeypatch, metric, bits):
                 sd, sr = gpu_search(eng, x, q, metric, k)
             np.testing.assert_array_equal(fr, sr)
             np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
+            with _lib.options(force_fallback=1):
+                gd, gr = gpu_search(eng, x, q, metric, k)
+            np.testing.assert_array_equal(gr, sr)
+            np.testing.assert_array_equal(gd.view(np.uint32), sd.view(np.uint32))
     assert not _lib.filter_image_used(n, d, _lib.DTYPE_F32, 1, k, _lib.METRICS[metric])
+    m = _lib.METRICS[metric]
+    big = (10_000_000, 768)  # 30.7 GB: >= 4 GiB
+    assert _lib.filter_image_used(*big, _lib.DTYPE_F32, 1, k, m)  # (defaults: int8 image)
+    with _lib.options(filter_image=16):
+        assert not _lib.filter_image_used(*big, _lib.DTYPE_F32, 1, k, m)
+    with _lib.options(single_query_image=0):
+        assert not _lib.filter_image_used(*big, _lib.DTYPE_F32, 1, k, m)
+    assert not _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, k, m)
 
 
 def test_filter_image_follows_corpus_changes(eng, monkeypatch):
