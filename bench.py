@@ -262,7 +262,7 @@ def main():
     # per corpus version: timed here, apart from the steps (reported in the
     # record's filter_image field)
     image_build_ms = None
-    if not qu8 and args.dtype == "f32":
+    if not qu8:
         b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         b0.record()
         built = eng.filter_image(shard, nq, k, metric)[0] is not None
@@ -311,7 +311,7 @@ def main():
     min_q = max(1, _lib.get_option("batch_min_queries"))
     batched = (_lib.get_option("batched") != 0 and nq >= min_q and not qu8
                and ((args.dtype == "f32" and d % 4 == 0) or (args.dtype == "f16" and d % 8 == 0)))
-    image = eng._images.get(id(x)) if args.dtype == "f32" and not qu8 else None
+    image = eng._images.get(id(x)) if not qu8 else None
     filt = batched or image is not None
     bits = image[0][3] if image is not None else 16
     if image is not None:

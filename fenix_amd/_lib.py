@@ -57,6 +57,7 @@ SYMBOLS = (
     "fx_knn_scan_img8",
     "fx_knn_search_img8",
     "fx_knn_reduce_img8",
+    "fx_filter_image8_typed",
     "fx_knn_distances",
     "fx_topk_merge_workspace_bytes",
     "fx_topk_merge",
@@ -159,6 +160,8 @@ def load() -> ctypes.CDLL:
         L.fx_filter_image8_bytes.restype = ci
         L.fx_filter_image8.argtypes = [vp, i64, i64, vp, vp, vp]
         L.fx_filter_image8.restype = ci
+        L.fx_filter_image8_typed.argtypes = [vp, ci, i64, i64, vp, vp, vp]
+        L.fx_filter_image8_typed.restype = ci
         L.fx_knn_scan_img8.argtypes = L.fx_knn_scan_img.argtypes
         L.fx_knn_scan_img8.restype = ci
         L.fx_knn_search_img8.argtypes = L.fx_knn_search_img.argtypes

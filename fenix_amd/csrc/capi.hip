@@ -220,8 +220,8 @@ static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool align
   // 2 queries: 6.5 ms vs 2 x 4.5 ms (10Mx768); "batch_min_queries" = 1 also
   // sends every single query through the filter
   int64_t min_q = option(kOptBatchMinQ) >= 1 ? option(kOptBatchMinQ) : 2;
-  if (nq == 1 && img8 && option(kOptSingleImage) != 0 && dtype == FX_DTYPE_F32 && d % 8 == 0 &&
-      n * d * 4 >= kSingleImageMinBytes)
+  if (nq == 1 && img8 && option(kOptSingleImage) != 0 && d % 8 == 0 &&
+      n * d * (dtype == FX_DTYPE_F32 ? 4 : 2) >= kSingleImageMinBytes)
     min_q = 1;
   if (!use_filter()) min_q = 8;  // the fp32-MFMA kernel breaks even with scans at ~8 queries
   if (nq < min_q || !aligned) return false;
@@ -704,10 +704,11 @@ static int search_layout(const void* corpus, int dtype, int64_t n, int64_t d, in
 
 }  // extern "C"
 
-// a filter image applies to f32 rows through the fp16 filter, with rows of
-// whole 16-B pieces (d % 8 == 0)
-static bool image_applies(const SearchLayout& s, int dtype, int64_t d) {
-  return s.batched && s.batch.filter && dtype == FX_DTYPE_F32 && d % 8 == 0;
+// a filter image applies to rows of whole 16-B pieces (d % 8 == 0) through
+// the filter: an fp16 image to f32 rows, an int8 image to f32 or f16 rows
+static bool image_applies(const SearchLayout& s, int dtype, int64_t d, bool img8) {
+  return s.batched && s.batch.filter && d % 8 == 0 &&
+         (dtype == FX_DTYPE_F32 || (img8 && dtype == FX_DTYPE_F16));
 }
 
 static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
@@ -730,7 +731,7 @@ static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (s.batched) {
     if (s.batch.filter) {
-      const bool img = image != nullptr && image_applies(s, dtype, d);
+      const bool img = image != nullptr && image_applies(s, dtype, d, img8);
       if (img && (rowinfo == nullptr || (uintptr_t)image % 16 != 0)) {
         set_error("filter image: null row info or image not 16-byte aligned");
         return FX_EINVAL;
@@ -868,6 +869,15 @@ int fx_filter_image8_bytes(int64_t n, int64_t d, size_t* image_bytes, size_t* ro
 
 int fx_filter_image8(const float* corpus, int64_t n, int64_t d, void* image, float* rowinfo,
                      void* stream) {
+  return fx_filter_image8_typed(corpus, FX_DTYPE_F32, n, d, image, rowinfo, stream);
+}
+
+int fx_filter_image8_typed(const void* corpus, int dtype, int64_t n, int64_t d, void* image,
+                           float* rowinfo, void* stream) {
+  if (dtype != FX_DTYPE_F32 && dtype != FX_DTYPE_F16) {
+    set_error("filter image: dtype %d is not float32 or float16", dtype);
+    return FX_EINVAL;
+  }
   size_t ib = 0, rb = 0;
   int rc = fx_filter_image8_bytes(n, d, &ib, &rb);
   if (rc) return rc;
@@ -883,7 +893,8 @@ int fx_filter_image8(const float* corpus, int64_t n, int64_t d, void* image, flo
     set_error("filter image: d=%lld too large", (long long)d);
     return FX_EUNSUPPORTED;
   }
-  return launch_image8(corpus, n, (int)d, image, rowinfo, reinterpret_cast<hipStream_t>(stream));
+  return launch_image8(corpus, dtype, n, (int)d, image, rowinfo,
+                       reinterpret_cast<hipStream_t>(stream));
 }
 
 int fx_filter_image_used(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
@@ -902,9 +913,10 @@ int fx_filter_image_used(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k,
   SearchLayout s;
   // (the int8 image, the host's default, also serves single queries over
   // large corpora: use_batched)
-  rc = plan_search(n, d, dtype, nq, k, metric, true, &s, option(kOptFilterImage) == 8);
+  const bool img8 = option(kOptFilterImage) == 8;
+  rc = plan_search(n, d, dtype, nq, k, metric, true, &s, img8);
   if (rc) return rc;
-  *out = image_applies(s, dtype, d) ? 1 : 0;
+  *out = image_applies(s, dtype, d, img8) ? 1 : 0;
   return FX_OK;
 }
 

@@ -187,7 +187,8 @@ bool image_tiled();
 constexpr int kI8RowInfo = 4;
 constexpr int kI8QInfo = 4;
 constexpr float kI8Kappa = 128.f;
-int launch_image8(const float* X, int64_t n, int d, void* img, float* rowinfo, hipStream_t stream);
+int launch_image8(const void* X, int dtype, int64_t n, int d, void* img, float* rowinfo,
+                  hipStream_t stream);
 int launch_qprep8(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
                   int8_t* Qb, float* qinfo, hipStream_t stream);
 int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,

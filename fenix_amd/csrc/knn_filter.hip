@@ -3477,7 +3477,11 @@ typedef float img_f32x16 __attribute__((ext_vector_type(16)));
 // 32-row tile: a pass for max |x| and n^2, a pass that quantizes, writes and
 // accumulates the residual (|x - s x~|^2 in f32 with (d + 8) u slack) and
 // w^2 (exact in integers).  d % 8 == 0 (fx_filter_image8 checks).
-__global__ void __launch_bounds__(256) image8_kernel(const float* __restrict__ X, int64_t n, int d,
+// T: the corpus's value type, float or _Float16 (the values are the same
+// reals in f32, so the bounds below are unchanged; the candidates are rescored
+// from the T rows in the scan's order)
+template <typename T>
+__global__ void __launch_bounds__(256) image8_kernel(const T* __restrict__ X, int64_t n, int d,
                                                     int8_t* __restrict__ img,
                                                     float* __restrict__ rowinfo) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
@@ -3488,19 +3492,31 @@ __global__ void __launch_bounds__(256) image8_kernel(const float* __restrict__ X
   for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < nt; t += nw) {
     const int64_t r = t * 32 + (lane & 31);
     const bool live = r < n;
-    const float* xr = X + (live ? r : 0) * (int64_t)d;
+    const T* xr = X + (live ? r : 0) * (int64_t)d;
     auto load = [&](int ks) {  // components 32 ks + 16 h .. + 15 (zeros past d)
       img_f32x16 v;
       const int k0 = 32 * ks + 16 * h;
+      if constexpr (sizeof(T) == 4) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + 4 * j;
-        const img_f32x4 q4 = (live && k < d) ? *reinterpret_cast<const img_f32x4*>(xr + k)
-                                              : img_f32x4(0.f);
-        v[4 * j] = q4[0];
-        v[4 * j + 1] = q4[1];
-        v[4 * j + 2] = q4[2];
-        v[4 * j + 3] = q4[3];
+        for (int j = 0; j < 4; ++j) {
+          const int k = k0 + 4 * j;
+          const img_f32x4 q4 = (live && k < d) ? *reinterpret_cast<const img_f32x4*>(xr + k)
+                                                : img_f32x4(0.f);
+          v[4 * j] = q4[0];
+          v[4 * j + 1] = q4[1];
+          v[4 * j + 2] = q4[2];
+          v[4 * j + 3] = q4[3];
+        }
+      } else {  // 8 halves per 16-B load (d % 8 == 0)
+        typedef _Float16 img_f16x8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int k = k0 + 8 * j;
+          const img_f16x8 h8 = (live && k < d) ? *reinterpret_cast<const img_f16x8*>(xr + k)
+                                                : img_f16x8((_Float16)0.f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[8 * j + e] = (float)h8[e];
+        }
       }
       return v;
     };
@@ -3561,7 +3577,7 @@ __global__ void __launch_bounds__(256) image8_kernel(const float* __restrict__ X
   }
 }
 
-int launch_image8(const float* X, int64_t n, int d, void* img, float* rowinfo,
+int launch_image8(const void* X, int dtype, int64_t n, int d, void* img, float* rowinfo,
                   hipStream_t stream) {
   if (n <= 0) return FX_OK;
   int cus = 0;
@@ -3569,8 +3585,14 @@ int launch_image8(const float* X, int64_t n, int d, void* img, float* rowinfo,
   if (rc) return rc;
   int64_t blocks = ((n + 31) / 32 + 3) / 4;
   if (blocks > (int64_t)cus * 8) blocks = (int64_t)cus * 8;
-  hipLaunchKernelGGL(image8_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, X, n, d,
-                     reinterpret_cast<int8_t*>(img), rowinfo);
+  if (dtype == FX_DTYPE_F16)
+    hipLaunchKernelGGL(image8_kernel<_Float16>, dim3((unsigned)blocks), dim3(256), 0, stream,
+                       reinterpret_cast<const _Float16*>(X), n, d, reinterpret_cast<int8_t*>(img),
+                       rowinfo);
+  else
+    hipLaunchKernelGGL(image8_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, stream,
+                       reinterpret_cast<const float*>(X), n, d, reinterpret_cast<int8_t*>(img),
+                       rowinfo);
   return check_launch("image8_kernel");
 }
 

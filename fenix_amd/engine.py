@@ -425,7 +425,7 @@ class Engine:
 
     def filter_image(self, shard: Shard, nq: int, k: int,
                      metric: int) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], int]:
-        """The filter image of an f32 shard for a search that runs the batched
+        """The filter image of an f32 (or, int8 images, f16) shard for a search that runs the batched
         filter (fx_filter_image_used): (image, rowinfo, bits), bits 8
         (fx_filter_image8, the default) or 16 (fx_filter_image) as the library
         option "filter_image" says, built on first use and kept while the
@@ -446,7 +446,9 @@ class Engine:
         stream waits for the build through an event recorded after it."""
         none = (None, None, 0)
         bits = _lib.get_option("filter_image")
-        if (shard.dtype_id != _lib.DTYPE_F32 or bits not in (8, 16)
+        # int8 images serve f32 and f16 corpora, fp16 images f32 ones
+        if ((shard.dtype_id != _lib.DTYPE_F32
+             and not (bits == 8 and shard.dtype_id == _lib.DTYPE_F16)) or bits not in (8, 16)
                 or os.environ.get("FENIX_AMD_FILTER_IMAGE", "1") == "0"
                 or not _lib.filter_image_used(shard.n, shard.d, shard.dtype_id, nq, k, metric)):
             return none
@@ -482,7 +484,11 @@ class Engine:
             info = torch.empty((rb.value // 4,), dtype=torch.float32, device=self.device)
         except torch.cuda.OutOfMemoryError:
             return none  # the f32 filter (no image) is always correct
-        _lib.check(build(_ptr(t), n, d, _ptr(img), _ptr(info), self._stream()))
+        if bits == 8:
+            _lib.check(L.fx_filter_image8_typed(_ptr(t), shard.dtype_id, n, d, _ptr(img),
+                                                _ptr(info), self._stream()))
+        else:
+            _lib.check(build(_ptr(t), n, d, _ptr(img), _ptr(info), self._stream()))
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self._images[key] = (sig, img, info, ev)

@@ -215,6 +215,11 @@ int fx_knn_search_img(const void* corpus, int dtype, int64_t n, int64_t d, int64
 int fx_filter_image8_bytes(int64_t n, int64_t d, size_t* image_bytes, size_t* rowinfo_bytes);
 int fx_filter_image8(const float* corpus, int64_t n, int64_t d, void* image, float* rowinfo,
                      void* stream);
+/* The same image of a float32 or float16 corpus (dtype FX_DTYPE_F32 /
+ * FX_DTYPE_F16): an fp16 column's searches then stream 1 byte per component
+ * instead of 2 and rescore from the fp16 rows in the fp16 scan's order. */
+int fx_filter_image8_typed(const void* corpus, int dtype, int64_t n, int64_t d, void* image,
+                           float* rowinfo, void* stream);
 int fx_knn_scan_img8(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,
                      const void* image, const float* rowinfo, const float* queries, int64_t nq,
                      int metric, int64_t k, const uint32_t* mask, void* ws, size_t ws_bytes,

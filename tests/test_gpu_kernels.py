@@ -762,7 +762,7 @@ def test_single_query_through_filter_image(eng, monkeypatch, metric, bits):
     the image (64-query tiles, one live query) and still equal the scan bit
     for bit, also through the overflow fallback ("force_fallback": the
     single query rescanned at the full scan's width).  By default a single
-    query takes the int8 image only over a >= 4 GiB f32 corpus
+    query takes the int8 image only over a >= 4 GiB f32 or f16 corpus
     ("single_query_image")."""
     n, d, k = 80_000, 256, 100
     xh = _extreme_rows(n, d, 45)
@@ -790,7 +790,10 @@ def test_single_query_through_filter_image(eng, monkeypatch, metric, bits):
         assert not _lib.filter_image_used(*big, _lib.DTYPE_F32, 1, k, m)
     with _lib.options(single_query_image=0):
         assert not _lib.filter_image_used(*big, _lib.DTYPE_F32, 1, k, m)
-    assert not _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, k, m)
+    # an fp16 column takes the int8 image too (>= 4 GiB of fp16 rows), never an fp16 image
+    assert _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, k, m)
+    with _lib.options(filter_image=16):
+        assert not _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, k, m)
 
 
 def test_filter_image_follows_corpus_changes(eng, monkeypatch):
