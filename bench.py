@@ -323,19 +323,23 @@ def main():
     # the filter image only): option single_query_image=0, same steps
     exact_scan = None
     if image is not None and nq == 1:
+        def local_step():  # this rank's search only (no collective: ranks may differ here)
+            ws = eng.scan(shard, q, metric, k)
+            eng.reduce(shard, q, metric, k, ws, od, orow)
+
         with _lib.options(single_query_image=0):
             for _ in range(2):
-                step()
+                local_step()
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             for _ in range(args.steps):
-                step()
+                local_step()
             torch.cuda.synchronize()
             xs_ms = (time.perf_counter() - t1) * 1e3 / args.steps
         xs_bytes = n * d * esize + nq * d * 4
-        exact_scan = {"ms_per_step": xs_ms, "vectors_per_s": n * world * nq / (xs_ms * 1e-3),
+        exact_scan = {"ms_per_step": xs_ms, "vectors_per_s": n * nq / (xs_ms * 1e-3),
                       "hbm_frac": xs_bytes / (xs_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                      "note": "the exact fused f32 scan + merge of the same query "
+                      "note": "this rank's exact fused scan + merge of the same query "
                               "(option single_query_image=0), the path of rounds 1-2"}
 
     achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
