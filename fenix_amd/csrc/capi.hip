@@ -213,14 +213,19 @@ static bool use_filter() { return diag_env("FX_BATCH_FILTER", 1) != 0; }
 // points, option "single_query_image"): 10M x 768 1.41 vs 4.34 ms; the
 // filter path's fixed cost (~0.25 ms of small launches) loses below ~2.4 GB
 static constexpr int64_t kSingleImageMinBytes = (int64_t)4 << 30;
+// The int8 image's bounds are wide: with k = 1 000 the final phase of a
+// 6.25M x 1536 fp16 IP search appended more than its 64 K candidate slots for
+// most queries (Flight, profiles/r03_f16_int8_image.log), and each overflow
+// costs a full rescan.  Int8 images serve k <= kI8MaxK only.
+static constexpr int64_t kI8MaxK = 256;
 
 static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool aligned, int64_t n,
-                        bool img8) {
+                        bool img8, int64_t k) {
   if (option(kOptBatched) == 0) return false;
   // 2 queries: 6.5 ms vs 2 x 4.5 ms (10Mx768); "batch_min_queries" = 1 also
   // sends every single query through the filter
   int64_t min_q = option(kOptBatchMinQ) >= 1 ? option(kOptBatchMinQ) : 2;
-  if (nq == 1 && img8 && option(kOptSingleImage) != 0 && d % 8 == 0 &&
+  if (nq == 1 && img8 && k <= kI8MaxK && option(kOptSingleImage) != 0 && d % 8 == 0 &&
       n * d * (dtype == FX_DTYPE_F32 ? 4 : 2) >= kSingleImageMinBytes)
     min_q = 1;
   if (!use_filter()) min_q = 8;  // the fp32-MFMA kernel breaks even with scans at ~8 queries
@@ -386,7 +391,7 @@ static int plan_fallback(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k,
 static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, int metric,
                        bool aligned, SearchLayout* s, bool img8 = false) {
   if (k > kMaxK) return plan_large_search(n, d, dtype, nq, metric, aligned, s);
-  if (!use_batched(nq, dtype, metric, d, aligned, n, img8)) {
+  if (!use_batched(nq, dtype, metric, d, aligned, n, img8, k)) {
     return plan_single(n, d, dtype, nq, k, metric, aligned, s);
   }
   // the single-query plan over fb_queries queries serves overflowing queries
@@ -706,7 +711,8 @@ static int search_layout(const void* corpus, int dtype, int64_t n, int64_t d, in
 
 // a filter image applies to rows of whole 16-B pieces (d % 8 == 0) through
 // the filter: an fp16 image to f32 rows, an int8 image to f32 or f16 rows
-static bool image_applies(const SearchLayout& s, int dtype, int64_t d, bool img8) {
+static bool image_applies(const SearchLayout& s, int dtype, int64_t d, bool img8, int64_t k) {
+  if (img8 && k > kI8MaxK) return false;
   return s.batched && s.batch.filter && d % 8 == 0 &&
          (dtype == FX_DTYPE_F32 || (img8 && dtype == FX_DTYPE_F16));
 }
@@ -731,7 +737,7 @@ static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (s.batched) {
     if (s.batch.filter) {
-      const bool img = image != nullptr && image_applies(s, dtype, d, img8);
+      const bool img = image != nullptr && image_applies(s, dtype, d, img8, k);
       if (img && (rowinfo == nullptr || (uintptr_t)image % 16 != 0)) {
         set_error("filter image: null row info or image not 16-byte aligned");
         return FX_EINVAL;
@@ -916,7 +922,7 @@ int fx_filter_image_used(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k,
   const bool img8 = option(kOptFilterImage) == 8;
   rc = plan_search(n, d, dtype, nq, k, metric, true, &s, img8);
   if (rc) return rc;
-  *out = image_applies(s, dtype, d, img8) ? 1 : 0;
+  *out = image_applies(s, dtype, d, img8, k) ? 1 : 0;
   return FX_OK;
 }
 

@@ -740,11 +740,16 @@ def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k, bits)
     q[0] *= 2.0 ** 50
     q[min(1, nq - 1)] = xh[7] if nq > 1 else q[0]
     monkeypatch.delenv("FENIX_AMD_FILTER_IMAGE", raising=False)
-    assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, nq, k, _lib.METRICS[metric])
     eng.clear_images()
     with _lib.options(filter_image=bits):
+        # (int8 images serve k <= 256: capi.hip kI8MaxK)
+        used = _lib.filter_image_used(n, d, _lib.DTYPE_F32, nq, k, _lib.METRICS[metric])
+        assert used == (bits == 16 or k <= 256)
         id_, ir = gpu_search(eng, x, q, metric, k)  # MFMA-fragment-order image
-    assert eng._images[id(x)][0][3] == bits  # the image path ran
+    if used:
+        assert eng._images[id(x)][0][3] == bits  # the image path ran
+    else:
+        assert id(x) not in eng._images
     eng.clear_images()
     monkeypatch.setenv("FENIX_AMD_FILTER_IMAGE", "0")
     nd, nr = gpu_search(eng, x, q, metric, k)
@@ -792,6 +797,9 @@ def test_single_query_through_filter_image(eng, monkeypatch, metric, bits):
         assert not _lib.filter_image_used(*big, _lib.DTYPE_F32, 1, k, m)
     # an fp16 column takes the int8 image too (>= 4 GiB of fp16 rows), never an fp16 image
     assert _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, k, m)
+    # k > 256: int8 bounds would overflow the candidate buffer (kI8MaxK)
+    assert not _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, 1000, m)
+    assert not _lib.filter_image_used(*big, _lib.DTYPE_F32, 1, 1000, m)
     with _lib.options(filter_image=16):
         assert not _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, k, m)
 
