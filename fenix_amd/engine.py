@@ -423,8 +423,8 @@ class Engine:
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    def filter_image(self, shard: Shard, nq: int, k: int,
-                     metric: int) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], int]:
+    def filter_image(self, shard: Shard, nq: int, k: int, metric: int, build: bool = True
+                     ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], int]:
         """The filter image of an f32 (or, int8 images, f16) shard for a search that runs the batched
         filter (fx_filter_image_used): (image, rowinfo, bits), bits 8
         (fx_filter_image8, the default) or 16 (fx_filter_image) as the library
@@ -465,6 +465,8 @@ class Engine:
             RESIDENT.touch(rkey)
             torch.cuda.current_stream(self.device).wait_event(hit[3])
             return hit[1], hit[2], bits
+        if not build:  # (reduce: only the image its scan used, never a new one)
+            return none
         self.invalidate_image(t)  # a stale image: free it before building the new one
         n, d = shard.n, shard.d
         L = _lib.load()
@@ -567,7 +569,7 @@ class Engine:
         fx_knn_reduce_img8 with the same image (the library may have planned a
         single query through the filter)."""
         nq = queries.shape[0]
-        img, _, bits = self.filter_image(shard, nq, k, metric)
+        img, _, bits = self.filter_image(shard, nq, k, metric, build=False)
         L = _lib.load()
         if bits == 8 and img is not None:
             _lib.check(L.fx_knn_reduce_img8(
