@@ -5,15 +5,26 @@ Workload (BASELINE.json configs[1], the headline metric's config): one query,
 "step" = one exact search over every row of this rank's shard, merge to the
 final sorted k, and for N > 1 the RCCL all-gather of the per-rank top-k plus
 the final merge (weak scaling: 10M rows per GPU, so N=8 is configs[3], 80M
-rows).  The search is the product default: for a >= 4 GiB f32 shard it
-streams the resident int8 filter image (built once per corpus version, timed
-apart as filter_image.build_ms) through the int8-MFMA bound filter and
-rescores the candidates from the f32 rows, bit-identical to the exact fused
-scan, which the record times beside it (exact_scan).
+rows).
+
+The headline (``value``, ``ms_per_step``, ``roofline``) is the exact fused
+f32 scan that reads every row, SURVEY §8(d): 3 072 B per vector, 30.72 GB per
+search.  The product default for the same single query streams a resident
+int8 filter image instead and rescores its candidates exactly (bit-identical
+results); it is timed as a second leg and reported under
+``accelerated_exact`` with the image's own bytes.  Batches (``--nq`` > 1,
+configs[2]) run the product path in the headline, priced over the image bytes
+(``roofline.bytes_basis``).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rows ROWS] [--d D]
                     [--k K] [--nq Q] [--metric l2|cosine|inner_product]
-                    [--dtype f32|f16] [--no-cpu-baseline]
+                    [--dtype f32|f16|qu8] [--cluster C] [--query normal|near]
+                    [--no-accelerated] [--no-cpu-baseline]
+
+Every leg checks its result: sorted and complete, one planted row per rank
+returned first in rank order (global row numbering), for N > 1 the merge
+equal to the host's merge of the gathered lists, and the accelerated leg
+equal to the exact scan bit for bit.
 
 ``--gpus N`` under a launcher (torch.distributed.run sets WORLD_SIZE) must
 equal the world size; without one, N > 1 starts the N ranks itself (a
@@ -58,7 +69,13 @@ def parse():
                    help="qu8: quint8 codes (ex/arrow/quint8), scanned by fx_knn_search_ex")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true",
-                   help="skip the sortedness check (diagnostic builds that drop work)")
+                   help="skip the result checks and the planted rows (diagnostic builds)")
+    p.add_argument("--no-accelerated", action="store_true",
+                   help="skip the filter-image leg (profiling the exact scan alone)")
+    p.add_argument("--cluster", type=int, default=0,
+                   help="rows clustered per C rows, x + 10 x0 (tests/test_flight.py:21-22)")
+    p.add_argument("--query", default="normal", choices=["normal", "near"],
+                   help="near: the query is corpus row n/3 + N(0,1)/2")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -138,7 +155,7 @@ QU8_SCALE = float(np.float32(4 * 3**0.5 / 127))
 QU8_ZP = 64
 
 
-def pmc_traffic(workload_tag, lib_sha):
+def pmc_traffic(workload_tag, kernel, lib_sha):
     """HBM bytes per scan launch from a committed rocprofv3 --pmc summary
     (profiles/*pmc*.json, FETCH_SIZE x2 gfx950 correction already applied,
     tools/summarize_profiles.py) of THIS build: the summary must carry the
@@ -151,7 +168,7 @@ def pmc_traffic(workload_tag, lib_sha):
         except (OSError, ValueError):
             continue
         if (rec.get("workload") == workload_tag and "hbm_bytes_per_launch" in rec
-                and rec.get("library_sha") == lib_sha):
+                and kernel in rec.get("kernel", "") and rec.get("library_sha") == lib_sha):
             return float(rec["hbm_bytes_per_launch"])
     return None
 
@@ -175,6 +192,38 @@ def launch_ranks(args) -> int:
            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
            "--master-port", str(free_port()), os.path.abspath(__file__), *sys.argv[1:]]
     return subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")).returncode
+
+
+def plant_rows(x: torch.Tensor, q: torch.Tensor, metric: str, rank: int, world: int):
+    """Plant one row per rank that must rank ``rank``-th of the merged top-k:
+    L2 / cosine: q + (rank+1)/16 e_0 (distance (rank+1)/16 for L2, growing
+    with the offset for cosine); inner product: (1000 - rank) q.  Returns the
+    local row.  (One row of the shard: the workload is unchanged otherwise.)"""
+    p = (rank * 7919 + 12345) % x.shape[0]
+    v = q[0].to(torch.float32).clone()
+    if metric in ("inner_product", "dot"):
+        v = v * float(1000 - rank)
+    else:
+        v[0] += (rank + 1) / 16.0
+    x[p] = v.to(x.dtype)
+    return p
+
+
+def host_merge(gd: np.ndarray, gr: np.ndarray, k: int):
+    """(distance, row) merge of gathered [nq, parts, kin] lists on the host:
+    the order fx_topk_merge must reproduce bit for bit."""
+    nq = gd.shape[0]
+    od = np.empty((nq, k), np.float32)
+    orow = np.empty((nq, k), np.int64)
+    for i in range(nq):
+        dd = gd[i].ravel().astype(np.float64)
+        rr = gr[i].ravel()
+        keep = rr >= 0
+        dd, rr = dd[keep], rr[keep]
+        o = np.lexsort((rr, np.where(np.isnan(dd), np.inf, dd)))[:k]
+        od[i, : len(o)], orow[i, : len(o)] = dd[o], rr[o]
+        orow[i, len(o):] = -1
+    return od, orow
 
 
 def main():
@@ -223,46 +272,103 @@ def main():
         tmp = torch.empty((1_000_000, d), dtype=torch.float32, device=device)
         for s in range(0, n, tmp.shape[0]):
             m = min(tmp.shape[0], n - s)
-            eng.fill(tmp[:m], seed=0, row_base=row_base + s)
+            eng.fill(tmp[:m], seed=0, row_base=row_base + s, cluster=args.cluster)
             x[s : s + m] = torch.clamp(torch.round(tmp[:m] / QU8_SCALE) + QU8_ZP, 0, 127).to(tdt)
         del tmp
     else:
-        eng.fill(x, seed=0, row_base=row_base)
+        eng.fill(x, seed=0, row_base=row_base, cluster=args.cluster)
     qh = torch.empty((nq, d), dtype=torch.float32 if qu8 else tdt, device=device)
     eng.fill(qh, seed=1)
+    if args.query == "near":  # a query inside the corpus's distribution: row n/3 + N(0,1)/2
+        qh = (x[n // 3 : n // 3 + 1].to(torch.float32) + 0.5 * qh.to(torch.float32)).to(qh.dtype)
     q = qh.to(torch.float32)
+    planted = None
+    if not qu8 and not args.no_verify:
+        planted = plant_rows(x, q, args.metric, rank, world)
+        torch.autograd.graph.increment_version(x)
     shard = Shard(x, row_base, QU8_SCALE, QU8_ZP) if qu8 else Shard(x, row_base)
     od = torch.empty((nq, k), dtype=torch.float32, device=device)
     orow = torch.empty((nq, k), dtype=torch.int64, device=device)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
 
-    def step(i=None):
-        if i is not None:
-            ev[i][0].record()
+    def step(ev=None):
+        """One search of this rank's shard (+ the all-gather and final merge
+        for N > 1); ``ev``: HIP events bracketing the scan launches on the
+        stream they are queued on."""
+        if ev is not None:
+            ev[0].record()
         if qu8:  # fx_knn_search_ex: scan + merge in one call (the merge is ~1 % of it)
             with eng.lock:
                 eng.search_shard(shard, q, metric, k, None, od, orow)
         else:
-            ws = eng.scan(shard, q, metric, k)
-        if i is not None:
-            ev[i][1].record()
+            st = eng.scan(shard, q, metric, k)
+        if ev is not None:
+            ev[1].record()
         if not qu8:
-            eng.reduce(shard, q, metric, k, ws, od, orow)
+            eng.reduce(shard, q, metric, k, st, od, orow)
         if use_dist:
             if gloo:
                 gd, gr = allgather_topk(od.cpu(), orow.cpu())
                 gd, gr = gd.to(device), gr.to(device)
             else:
                 gd, gr = allgather_topk(od, orow)  # one RCCL all-gather over xGMI
-            return eng.merge(gd, gr, k)
-        return od, orow
+            md, mr = eng.merge(gd, gr, k)
+            return md, mr, gd, gr
+        return od.clone(), orow.clone(), None, None
 
-    # a batched f32 search streams the corpus's filter image, built once
-    # per corpus version: timed here, apart from the steps (reported in the
-    # record's filter_image field)
+    def timed_leg():
+        """W untimed warmup steps, then exactly K steps bracketed by a barrier
+        and a device synchronisation on both sides; (elapsed s max over ranks,
+        mean event-timed scan span ms max over ranks, last result)."""
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if use_dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            res = step(ev[i])
+        torch.cuda.synchronize()
+        if use_dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        span = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        if use_dist:
+            t = torch.tensor([elapsed, span], dtype=torch.float64, device="cpu" if gloo else device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed, span = float(t[0]), float(t[1])
+        return elapsed, span, res
+
+    def verify(res, what):
+        """Sorted and complete; the planted rows first, in rank order; for
+        N > 1 the merge equals the host's (distance, row) merge of the
+        gathered lists, bit for bit."""
+        if args.no_verify:
+            return
+        rd, rr = res[0].cpu().numpy(), res[1].cpu().numpy()
+        assert (rr >= 0).all() and np.all(np.diff(rd, axis=1) >= 0), f"{what}: result not sorted"
+        if planted is not None and k >= world:
+            want = np.array([g * n + (g * 7919 + 12345) % n for g in range(world)])
+            assert (rr[0, :world] == want).all(), f"{what}: planted rows {rr[0, :world]} != {want}"
+        if res[2] is not None:
+            hd, hr = host_merge(res[2].cpu().numpy(), res[3].cpu().numpy(), k)
+            assert np.array_equal(hr, rr) and np.array_equal(hd.view(np.uint32),
+                                                             rd.view(np.uint32)), \
+                f"{what}: device merge differs from the host merge of the gathered lists"
+
+    # the filter image (int8 by default) of the product path, built once per
+    # corpus version before any timing: batches stream it in the headline
+    # leg, a single query in the accelerated leg
+    single = nq == 1 and not qu8
+    image = None
     image_build_ms = None
-    if not qu8:
+    img_bytes = None
+    want_image = not qu8 and not (single and args.no_accelerated) and \
+        _lib.filter_image_used(n, d, shard.dtype_id, nq, k, metric)
+    if want_image:
         b0, b1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         b0.record()
         built = eng.filter_image(shard, nq, k, metric)[0] is not None
@@ -270,79 +376,60 @@ def main():
         torch.cuda.synchronize()
         if built:
             image_build_ms = b0.elapsed_time(b1)
+            image = eng._images.get(id(x))
+            img_bytes = int(image[1].numel()) * image[1].element_size() + \
+                int(image[2].numel()) * 4
+    bits = image[0][3] if image is not None else 16
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        res = step(i)
-    torch.cuda.synchronize()
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    scan_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if use_dist:
-        t = torch.tensor([elapsed, scan_ms], dtype=torch.float64,
-                         device="cpu" if gloo else device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, scan_ms = float(t[0]), float(t[1])
+    # The headline: a single query runs the exact fused scan
+    # over every row (option single_query_image=0); batches run the product
+    # path (the bound filter over the filter image).
+    with _lib.options(single_query_image=0) if single else _nullctx():
+        elapsed, scan_ms, res = timed_leg()
+    verify(res, "headline")
 
-    # sanity: the last result is sorted and complete
-    rd, rr = res[0].cpu().numpy(), res[1].cpu().numpy()
-    assert args.no_verify or (rr >= 0).all() and np.all(np.diff(rd, axis=1) >= 0), \
-        "bench result not sorted"
+    # the product default for the same single query: the int8 filter image +
+    # exact rescoring (bit-identical), timed as its own leg
+    accel = None
+    if single and image is not None:
+        head = res
+        a_el, a_ms, res = timed_leg()
+        verify(res, "accelerated")
+        same = bool(np.array_equal(head[1].cpu().numpy(), res[1].cpu().numpy()) and np.array_equal(
+            head[0].cpu().numpy().view(np.uint32), res[0].cpu().numpy().view(np.uint32)))
+        if not args.no_verify:
+            assert same, "the filter-image search differs from the exact scan"
+        pass_bytes = img_bytes + nq * d * 4
+        a_traffic = pmc_traffic(f"{n}x{d}_{args.dtype}_{args.metric}_k{k}_q{nq}", "filter_img3",
+                                _lib.library_sha())
+        accel = {
+            "what": "the product default for this search: int8 filter image + exact rescoring "
+                    "of the candidates from the f32 rows (capi.hip filter_phases)",
+            "ms_per_step": a_el * 1e3 / args.steps,
+            "vectors_per_s": n * world * nq * args.steps / a_el,
+            "kernel_ms": a_ms,
+            "kernel": "fx::q64i::filter_img3_kernel (all phases) + thresholds + rescoring",
+            "image_bytes": img_bytes,
+            "image_build_ms": image_build_ms,
+            "bytes_per_search": pass_bytes,
+            "achieved_gbs_over_image": pass_bytes / (a_ms * 1e-3) / 1e9,
+            "frac_over_image": pass_bytes / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "traffic": a_traffic,
+            "traffic_over_image": (a_traffic / pass_bytes) if a_traffic else None,
+            "bit_identical": same,
+            "speedup_vs_headline": elapsed / a_el,
+        }
 
     total_rows = n * world
     value = total_rows * nq * args.steps / elapsed
     scan_bytes = n * d * esize + nq * d * 4
+    algo_bytes = scan_bytes
     tag = f"{n}x{d}_{args.dtype}_{args.metric}_k{k}_q{nq}"
-    traffic = pmc_traffic(tag, _lib.library_sha())
-    # batched queries: the MFMA bound filter + exact rescoring
-    # (knn_filter.hip), one HBM-bound pass over the corpus (capi.hip
-    # use_batched: from "batch_min_queries" queries, f32 rows with d % 4 == 0,
-    # f16 rows with d % 8 == 0; a single query over a >= 4 GiB f32 corpus
-    # when the engine supplies an int8 filter image, which it builds exactly
-    # when the library will read it: fx_filter_image_used)
-    min_q = max(1, _lib.get_option("batch_min_queries"))
-    batched = (_lib.get_option("batched") != 0 and nq >= min_q and not qu8
-               and ((args.dtype == "f32" and d % 4 == 0) or (args.dtype == "f16" and d % 8 == 0)))
-    image = eng._images.get(id(x)) if not qu8 else None
-    filt = batched or image is not None
-    bits = image[0][3] if image is not None else 16
-    if image is not None:
-        # the phases stream the filter image and its row terms instead of the
-        # f32 rows: those are the bytes of the pass (the rescoring reads a
-        # few thousand f32 rows per query on top)
-        scan_bytes = n * d * bits // 8 + n * (16 if bits == 8 else 4) + nq * d * 4
-    # the exact f32 scan of the same search beside it (single queries through
-    # the filter image only): option single_query_image=0, same steps
-    exact_scan = None
-    if image is not None and nq == 1:
-        def local_step():  # this rank's search only (no collective: ranks may differ here)
-            ws = eng.scan(shard, q, metric, k)
-            eng.reduce(shard, q, metric, k, ws, od, orow)
-
-        with _lib.options(single_query_image=0):
-            for _ in range(2):
-                local_step()
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            for _ in range(args.steps):
-                local_step()
-            torch.cuda.synchronize()
-            xs_ms = (time.perf_counter() - t1) * 1e3 / args.steps
-        xs_bytes = n * d * esize + nq * d * 4
-        exact_scan = {"ms_per_step": xs_ms, "vectors_per_s": n * nq / (xs_ms * 1e-3),
-                      "hbm_frac": xs_bytes / (xs_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                      "note": "this rank's exact fused scan + merge of the same query "
-                              "(option single_query_image=0), the path of rounds 1-2"}
-
-    achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
+    filt = not single and not qu8 and image is not None
+    if filt:
+        # a batch streams the filter image and its row terms instead of the
+        # rows (the rescoring reads a few thousand rows per query on top)
+        scan_bytes = img_bytes + nq * d * 4
     if filt:
         kname = (f"fx::filter_img3_kernel ({'int8' if bits == 8 else 'fp16'}-MFMA bound filter, "
                  "all sample phases) + exact rescoring of the candidates")
@@ -350,6 +437,8 @@ def main():
         kname = "fx::scan_kernel<uint8> (quint8 codes dequantised in registers) + merge"
     else:
         kname = "fx::scan_kernel (fused distance + per-wave top-k)"
+    traffic = pmc_traffic(tag, "filter_img3" if filt else "scan_kernel", _lib.library_sha())
+    achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
     roof = {
         "bound": "hbm",
         "achieved": achieved,
@@ -362,6 +451,8 @@ def main():
         "library_sha": _lib.library_sha(),
     }
     if filt:  # the GEMM the filter evaluates, against the dense MFMA peak of its type
+        roof["bytes_basis"] = "filter image + row terms (the pass reads these, not the rows)"
+        roof["algorithmic_bytes"] = algo_bytes
         roof["mfma_tflops"] = 2.0 * n * nq * d / (scan_ms * 1e-3) / 1e12
         roof["mfma_peak_tflops"] = MFMA_F16_PEAK_TFS * (2 if bits == 8 else 1)
     roof["frac"] = roof["achieved"] / roof["peak"]
@@ -371,7 +462,8 @@ def main():
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
         wl = (f"{n // 1_000_000 if n % 1_000_000 == 0 else n}"
               f"{'M' if n % 1_000_000 == 0 else ''}x{d} {args.dtype} {args.metric.upper()} "
-              f"kNN k={k}, {'single query' if nq == 1 else f'{nq}-query batch'}, per GPU")
+              f"kNN k={k}, {'single query' if nq == 1 else f'{nq}-query batch'}, per GPU"
+              + (f", clustered x{args.cluster}" if args.cluster else ""))
         out = {
             "metric": METRIC,
             "value": value,
@@ -385,35 +477,34 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic: portable Irwin-Hall(4) N(0,1) generator on device "
-                    "(corpus seed 0, query seed 1), corpus resident in HBM",
+                    "(corpus seed 0, query seed 1), corpus resident in HBM"
+                    + (f"; rows clustered per {args.cluster} (x + 10 x0, test_flight.py:21-22)"
+                       if args.cluster else "")
+                    + ("; query = row n/3 + N(0,1)/2" if args.query == "near" else "")
+                    + ("" if planted is None else "; one planted row per rank (verified first)"),
             "config": {
                 "workload": wl,
+                "path": ("exact fused f32 scan over every row (SURVEY 8(d))" if single
+                         else "bound filter over the filter image + exact rescoring"
+                         if filt else "exact fused scan"),
                 "rows_per_gpu": n,
                 "total_rows": total_rows,
                 "d": d,
                 "k": k,
                 "queries": nq,
                 "metric": args.metric,
+                **({"cluster": args.cluster} if args.cluster else {}),
+                **({"query": args.query} if args.query != "normal" else {}),
                 **({"options": args.opt} if args.opt else {}),
                 "parallelism": f"row-shard x{world}"
                 + ((" + gloo all-gather" if gloo else " + RCCL all-gather") if use_dist else ""),
             },
-            # the batched filter streamed the corpus's resident filter image
-            # (fx_filter_image8 / fx_filter_image, built before the warmup;
-            # candidates rescored from the f32 rows, results bit-identical to
-            # the f32 scan)
-            **({"filter_image": {"bits": bits,
-                                 "bytes": int(image[1].numel()) * image[1].element_size()
-                                 + int(image[2].numel()) * 4,
-                                 "build_ms": image_build_ms,
-                                 "note": f"{'int8' if bits == 8 else 'fp16'} image + per-row "
-                                         "bound terms resident beside the f32 corpus, built "
-                                         "once per corpus version (build_ms, not in "
-                                         "ms_per_step); option filter_image=16 or 0 selects "
-                                         "fp16 or none"}}
+            **({"filter_image": {"bits": bits, "bytes": img_bytes, "build_ms": image_build_ms,
+                                 "note": "resident beside the corpus, built once per corpus "
+                                         "version (not in ms_per_step)"}}
                if image is not None else {}),
             "roofline": roof,
-            **({"exact_scan": exact_scan} if exact_scan is not None else {}),
+            **({"accelerated_exact": accel} if accel is not None else {}),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
@@ -421,6 +512,14 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return out
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
 
 
 if __name__ == "__main__":

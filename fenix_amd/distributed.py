@@ -55,10 +55,20 @@ def allgather_topk(
 
 def sharded_search(engine, shard, queries: torch.Tensor, metric: int, k: int,
                    group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Local fused scan on this rank's shard, all-gather, deterministic merge."""
+    """Local fused scan on this rank's shard, all-gather, deterministic merge.
+
+    ``shard.row_base`` must be the shard's first global row (``shard_rows``),
+    so the merged rows are positions in the concatenated table.  Over a gloo
+    group (CPU tests, several ranks sharing one GPU) the k lists travel
+    through host memory; over RCCL they stay on the device."""
     d_loc, r_loc = engine.search([shard], queries, metric, k)
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return d_loc, r_loc
-    d_all, r_all = allgather_topk(d_loc, r_loc, group)
+    if dist.get_backend(group) == "gloo" and d_loc.is_cuda:
+        dev = d_loc.device
+        d_all, r_all = allgather_topk(d_loc.cpu(), r_loc.cpu(), group)
+        d_all, r_all = d_all.to(dev), r_all.to(dev)
+    else:
+        d_all, r_all = allgather_topk(d_loc, r_loc, group)
     with engine.lock:
         return engine.merge(d_all, r_all, k)

@@ -178,6 +178,17 @@ class Piece:
 
 
 @dataclass
+class ScanState:
+    """What ``Engine.scan`` hands to ``Engine.reduce``: the workspace and the
+    filter image (None: the scan read none) with its width in bits."""
+
+    ws: torch.Tensor
+    image: Optional[torch.Tensor]
+    rowinfo: Optional[torch.Tensor]
+    bits: int
+
+
+@dataclass
 class _Entry:
     key: tuple
     table: pa.Table
@@ -266,18 +277,21 @@ class Residency:
         with self._lock:
             self._items.pop(key, None)
 
-    def reserve(self, need: Dict[int, int], keep: Sequence[tuple] = ()) -> bool:
-        """Evict until ``need`` more bytes fit every listed device's budget;
-        False when they cannot (everything evictable is gone).  The victims'
-        callbacks run after this object's lock is released (they take their
-        cache's lock)."""
+    def reserve(self, need: Dict[int, int], keep: Sequence[tuple] = (),
+                kinds: Sequence[int] = (0, 1)) -> bool:
+        """Evict entries of ``kinds`` (LRU first, images before corpora) until
+        ``need`` more bytes fit every listed device's budget; False when they
+        cannot.  A filter image reserves with ``kinds=(IMAGE,)``: an optional
+        image never evicts a corpus (it could be the one it is built for).
+        The victims' callbacks run after this object's lock is released (they
+        take their cache's lock)."""
         victims = []
         ok = True
         with self._lock:
             for dev, extra in need.items():
                 budget = _budget_bytes(dev)
                 used = self.used(dev)
-                for kind in (self.IMAGE, self.CORPUS):
+                for kind in [k for k in (self.IMAGE, self.CORPUS) if k in kinds]:
                     for key in [k for k, v in self._items.items()
                                 if v[0] == kind and v[1].get(dev, 0) > 0 and k not in keep]:
                         if used + extra <= budget:
@@ -430,8 +444,8 @@ class Engine:
         (fx_filter_image8, the default) or 16 (fx_filter_image) as the library
         option "filter_image" says, built on first use and kept while the
         corpus tensor lives and is unmodified; (None, None, 0) when the search
-        does not read one, when the option is 0 (or ``FENIX_AMD_FILTER_IMAGE=0``),
-        or when the HBM budget (``Residency``) cannot hold it.  The filter only
+        does not read one, when the option is 0, or when the HBM budget
+        (``Residency``) cannot hold it without evicting a corpus.  The filter only
         selects candidates, which are rescored from the f32 rows, so results
         never depend on whether or which image is used.
 
@@ -443,13 +457,14 @@ class Engine:
         ``invalidate_image`` afterwards.
 
         The image is built on the caller's current stream; a search on another
-        stream waits for the build through an event recorded after it."""
+        stream waits for the build through an event recorded after it, and the
+        image is recorded on that stream, so an eviction while the search runs
+        cannot hand its memory to another allocation early."""
         none = (None, None, 0)
         bits = _lib.get_option("filter_image")
         # int8 images serve f32 and f16 corpora, fp16 images f32 ones
         if ((shard.dtype_id != _lib.DTYPE_F32
              and not (bits == 8 and shard.dtype_id == _lib.DTYPE_F16)) or bits not in (8, 16)
-                or os.environ.get("FENIX_AMD_FILTER_IMAGE", "1") == "0"
                 or not _lib.filter_image_used(shard.n, shard.d, shard.dtype_id, nq, k, metric)):
             return none
         t = shard.data
@@ -463,19 +478,21 @@ class Engine:
         hit = self._images.get(key)
         if hit is not None and hit[0] == sig:
             RESIDENT.touch(rkey)
-            torch.cuda.current_stream(self.device).wait_event(hit[3])
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(hit[3])
+            hit[1].record_stream(cur)
+            hit[2].record_stream(cur)
             return hit[1], hit[2], bits
         if not build:  # (reduce: only the image its scan used, never a new one)
             return none
         self.invalidate_image(t)  # a stale image: free it before building the new one
         n, d = shard.n, shard.d
         L = _lib.load()
-        sizes, build = ((L.fx_filter_image8_bytes, L.fx_filter_image8) if bits == 8
-                        else (L.fx_filter_image_bytes, L.fx_filter_image))
+        size_fn = L.fx_filter_image8_bytes if bits == 8 else L.fx_filter_image_bytes
         ib, rb = ctypes.c_size_t(0), ctypes.c_size_t(0)
-        _lib.check(sizes(n, d, ctypes.byref(ib), ctypes.byref(rb)))
+        _lib.check(size_fn(n, d, ctypes.byref(ib), ctypes.byref(rb)))
         need = ib.value + rb.value
-        if not RESIDENT.reserve({self.device.index: need}):
+        if not RESIDENT.reserve({self.device.index: need}, kinds=(Residency.IMAGE,)):
             return none
         free, _ = torch.cuda.mem_get_info(self.device)
         cached = torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
@@ -490,7 +507,7 @@ class Engine:
             _lib.check(L.fx_filter_image8_typed(_ptr(t), shard.dtype_id, n, d, _ptr(img),
                                                 _ptr(info), self._stream()))
         else:
-            _lib.check(build(_ptr(t), n, d, _ptr(img), _ptr(info), self._stream()))
+            _lib.check(L.fx_filter_image(_ptr(t), n, d, _ptr(img), _ptr(info), self._stream()))
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self._images[key] = (sig, img, info, ev)
@@ -524,6 +541,7 @@ class Engine:
         nbytes = _lib.knn_workspace_bytes(shard.n, shard.d, shard.dtype_id, nq, k)
         ws = self._workspace(nbytes)
         img, info, bits = self.filter_image(shard, nq, k, metric)
+        self._hold(shard.data)
         L = _lib.load()
         _lib.check(
             (L.fx_knn_search_img8 if bits == 8 else L.fx_knn_search_img)(
@@ -540,17 +558,33 @@ class Engine:
         c = shard.corpus()
         nq = queries.shape[0]
         ws = self._workspace(_lib.search_ex_workspace_bytes(c, nrows, nq, k))
+        self._hold(shard.data)
         _lib.check(_lib.load().fx_knn_search_ex(
             ctypes.byref(c), _ptr(rows), nrows, _ptr(queries), nq, metric, k, _ptr(mask),
             _ptr(ws), ws.numel(), _ptr(out_dist), _ptr(out_row), self._stream()))
 
+    def _hold(self, *tensors: Optional[torch.Tensor]) -> None:
+        """Record the current stream on cached tensors a launch reads (corpus
+        shards, filter images): if a cache evicts them while the kernels run on
+        a stream other than the one they were allocated on, the caching
+        allocator waits for this stream before reusing their memory."""
+        cur = torch.cuda.current_stream(self.device)
+        for t in tensors:
+            if t is not None and t.is_cuda:
+                t.record_stream(cur)
+
     def scan(self, shard: Shard, queries: torch.Tensor, metric: int, k: int,
-             mask: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Phase 1 of search_shard (fx_knn_scan): returns the workspace to reduce."""
+             mask: Optional[torch.Tensor] = None) -> "ScanState":
+        """Phase 1 of search_shard (fx_knn_scan / fx_knn_scan_img8): returns the
+        state ``reduce`` completes — the workspace and the exact filter image
+        (and its width) the scan planned with, held until the reduce, so the
+        pair never plans differently (an image evicted or rebuilt in between
+        would make fx_knn_reduce read a filter workspace as scan lists)."""
         nq = queries.shape[0]
         nbytes = _lib.knn_workspace_bytes(shard.n, shard.d, shard.dtype_id, nq, k)
         ws = self._workspace(nbytes)
         img, info, bits = self.filter_image(shard, nq, k, metric)
+        self._hold(shard.data)
         L = _lib.load()
         _lib.check(
             (L.fx_knn_scan_img8 if bits == 8 else L.fx_knn_scan_img)(
@@ -559,22 +593,22 @@ class Engine:
                 ws.numel(), self._stream(),
             )
         )
-        return ws
+        return ScanState(ws, img, info, bits)
 
-    def reduce(self, shard: Shard, queries: torch.Tensor, metric: int, k: int, ws: torch.Tensor,
+    def reduce(self, shard: Shard, queries: torch.Tensor, metric: int, k: int, state: "ScanState",
                out_dist: torch.Tensor, out_row: torch.Tensor,
                mask: Optional[torch.Tensor] = None) -> None:
-        """Phase 2 of search_shard (fx_knn_reduce), same arguments as scan.  A
-        scan that received an int8 filter image is completed by
-        fx_knn_reduce_img8 with the same image (the library may have planned a
-        single query through the filter)."""
+        """Phase 2 of search_shard (fx_knn_reduce), same arguments as scan plus
+        its state.  A scan that received an int8 filter image is completed by
+        fx_knn_reduce_img8 with that same image (the library may have planned
+        a single query through the filter)."""
         nq = queries.shape[0]
-        img, _, bits = self.filter_image(shard, nq, k, metric, build=False)
+        ws = state.ws
         L = _lib.load()
-        if bits == 8 and img is not None:
+        if state.bits == 8 and state.image is not None:
             _lib.check(L.fx_knn_reduce_img8(
-                _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base, _ptr(img),
-                _ptr(queries), nq, metric, k, _ptr(mask), _ptr(ws), ws.numel(),
+                _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base,
+                _ptr(state.image), _ptr(queries), nq, metric, k, _ptr(mask), _ptr(ws), ws.numel(),
                 _ptr(out_dist), _ptr(out_row), self._stream()))
             return
         _lib.check(
@@ -622,6 +656,7 @@ class Engine:
             self._search_ex(shard, rows, nrows, queries, metric, k, None, out_dist, out_row)
             return
         ws = self._workspace(_lib.search_rows_workspace_bytes(nrows, shard.d, shard.dtype_id, nq, k))
+        self._hold(shard.data)
         _lib.check(_lib.load().fx_knn_search_rows(
             _ptr(shard.data), shard.dtype_id, shard.n, shard.d, shard.row_base, _ptr(rows), nrows,
             _ptr(queries), nq, metric, k, _ptr(ws), ws.numel(), _ptr(out_dist), _ptr(out_row),

@@ -99,3 +99,84 @@ def test_gloo_world2_gather_and_merge():
     sd, sr = got[0]["special"]
     assert np.isnan(sd[0, 0, 0]) and np.signbit(sd[0, 0, 1]) and np.isinf(sd[0, 0, 2])
     assert list(sr[0, :, 0]) == [0, 1]
+
+
+class _HostEngine:
+    """Stand-in for fenix_amd.engine.Engine with the two calls sharded_search
+    makes (search, merge), computed by the CPU oracle and a host (distance,
+    row) merge: exercises the distributed control flow without a GPU."""
+
+    def __init__(self):
+        import threading
+
+        self.lock = threading.Lock()
+
+    def search(self, shards, queries, metric, k):
+        from oracle import oracle as O
+
+        (sh,) = shards
+        od, orow = O.knn(sh.data, queries.numpy(), sh.metric_name, k, row_base=sh.row_base,
+                         threads=1)
+        return torch.from_numpy(od.astype(np.float32)), torch.from_numpy(orow)
+
+    def merge(self, d, r, k):
+        d, r = d.numpy(), r.numpy()
+        outd = np.empty((d.shape[0], k), np.float32)
+        outr = np.empty((d.shape[0], k), np.int64)
+        for i in range(d.shape[0]):
+            dd, rr = d[i].ravel().astype(np.float64), r[i].ravel()
+            o = np.lexsort((rr, dd))[:k]
+            outd[i], outr[i] = dd[o], rr[o]
+        return torch.from_numpy(outd), torch.from_numpy(outr)
+
+
+def _sharded_worker(rank, world, port, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from types import SimpleNamespace
+
+        from fenix_amd.distributed import sharded_search
+        from oracle import oracle as O
+
+        n_total, d, k = 7003, 40, 30
+        base, n_local = shard_rows(n_total, world, rank)
+        q = torch.from_numpy(O.fill_normal(4, d, seed=5))
+        out = {}
+        for metric in ("l2", "cosine", "inner_product"):
+            sh = SimpleNamespace(data=O.fill_normal(n_local, d, seed=4, row_base=base),
+                                 row_base=base, metric_name=metric)
+            md, mr = sharded_search(_HostEngine(), sh, q, 0, k)
+            out[metric] = (md.numpy(), mr.numpy())
+        result_q.put((rank, out))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_gloo_world3_sharded_search_equals_whole():
+    """fenix_amd.distributed.sharded_search over 3 gloo ranks (uneven shards):
+    every rank returns the global top-k of the whole corpus, rows numbered
+    globally through each shard's row_base."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world = 3
+    port = _port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    from oracle import oracle as O
+
+    x_all = O.fill_normal(7003, 40, seed=4)
+    qv = O.fill_normal(4, 40, seed=5)
+    for metric in ("l2", "cosine", "inner_product"):
+        od, orow = O.knn(x_all, qv, metric, 30)
+        for r in range(world):
+            np.testing.assert_array_equal(got[r][metric][1], orow)
+            np.testing.assert_allclose(got[r][metric][0], od, rtol=1e-6, atol=1e-6)

@@ -296,6 +296,72 @@ def test_hbm_budget_evicts_and_restages(env, monkeypatch):
     engine.CACHE.clear()
 
 
+def test_configs0_100k_x128_l2_k10(env):
+    """BASELINE configs[0] at its workload: 100 000 x 128 float32 rows (i.i.d.
+    N(0,1), written by Flight.make_table in 1 000-row batches), L2, k = 10,
+    single queries, through io.index.call (index.py:81-170) and through
+    Flight.search (flight.py:242-288): ids bit-exact against the float64
+    oracle, distances within 1e-5 relative."""
+    root = env["root"]
+    x0 = O.fill_normal(100_000, 128, seed=1000)
+    sch = pa.schema({"id": pa.int64(), "vector": pa.list_(pa.float32(), 128)})
+    env["flight"].make_table("test/cfg0", pa.Table.from_batches(batches(x0), sch).to_reader())
+    targets = O.fill_normal(8, 128, seed=1001)
+    od, orow = O.knn(x0, targets, "l2", 10)
+    for i, t in enumerate(targets):
+        direct = index.call(root, None, "test/cfg0", "vector", target=t, metric="l2", maxval=10)
+        remote = env["flight"].search(target=t, source="test/cfg0", column="vector",
+                                      metric="euclidean" if i % 2 else "l2", maxval=10)
+        for r in (direct, remote):
+            assert r.num_rows == 10
+            assert r.schema == pa.schema([*sch, pa.field("__DISTANCE__", pa.float32())])
+            np.testing.assert_array_equal(r.column("id").to_numpy(), orow[i])
+            got = r.column("__DISTANCE__").to_numpy().astype(np.float64)
+            assert np.all(np.abs(got - od[i]) <= 1e-5 * np.abs(od[i]))
+            vec = np.stack(r.column("vector").to_numpy(zero_copy_only=False))
+            np.testing.assert_array_equal(vec, x0[orow[i]])
+
+
+def test_image_budget_never_evicts_its_corpus(env, monkeypatch):
+    """A budget between the staged corpus alone and corpus + filter image: the
+    optional image is not built (it never evicts a corpus, least of all the
+    one it is for), the corpus stays resident and the batched search still
+    equals the scan (image reservations evict images only)."""
+    from fenix_amd import _lib, engine
+
+    root = env["root"]
+    engine.CACHE.clear()
+    engine.RESIDENT.evict_all()
+    t = O.fill_normal(1, VECTOR_SIZE, seed=93)[0]
+    index.call(root, None, "test/table", "vector", target=t, metric="l2", maxval=5)
+    (entry,) = engine.CACHE._entries.values()
+    piece = entry.pieces[0]
+    col_bytes = NUM_VECTORS * VECTOR_SIZE * 4
+    monkeypatch.setenv("FENIX_AMD_HBM_BUDGET", str(int(col_bytes * 1.1)))  # image: +0.27x
+    eng = engine.Engine.get(piece.device)
+    eng.clear_images()
+    ev0 = engine.RESIDENT.evictions
+    qs = torch.from_numpy(O.fill_normal(16, VECTOR_SIZE, seed=94))
+    shard = engine.Shard(piece.data, 0)
+    assert _lib.filter_image_used(shard.n, shard.d, shard.dtype_id, 16, 50, _lib.METRIC_L2)
+    bd, br = eng.search([shard], qs, _lib.METRIC_L2, 50)
+    assert id(piece.data) not in eng._images  # no room: no image
+    assert engine.RESIDENT.evictions == ev0
+    assert entry.key in engine.CACHE
+    with _lib.options(batched=0):
+        sd, sr = eng.search([shard], qs, _lib.METRIC_L2, 50)
+    np.testing.assert_array_equal(br.cpu().numpy(), sr.cpu().numpy())
+    np.testing.assert_array_equal(bd.cpu().numpy().view(np.uint32),
+                                  sd.cpu().numpy().view(np.uint32))
+    monkeypatch.setenv("FENIX_AMD_HBM_BUDGET", str(int(col_bytes * 1.5)))
+    eng.search([shard], qs, _lib.METRIC_L2, 50)
+    assert id(piece.data) in eng._images  # room again: built, corpus still resident
+    assert entry.key in engine.CACHE and engine.RESIDENT.evictions == ev0
+    monkeypatch.delenv("FENIX_AMD_HBM_BUDGET")
+    eng.clear_images()
+    engine.CACHE.clear()
+
+
 def test_remove(env):
     flight = env["flight"]
     flight.remove()

@@ -480,11 +480,8 @@ def test_batched_filter_bit_identical_to_scan(eng, metric, n, d, nq, k):
     image is off here: test_filter_image_bit_identical covers it.)"""
     x = gpu_fill(eng, n, d, seed=21)
     q = O.fill_normal(nq, d, seed=22)
-    os.environ["FENIX_AMD_FILTER_IMAGE"] = "0"
-    try:
+    with _lib.options(filter_image=0):
         fd, fr = gpu_search(eng, x, q, metric, k)
-    finally:
-        del os.environ["FENIX_AMD_FILTER_IMAGE"]
     with _lib.options(batched=0):
         sd, sr = gpu_search(eng, x, q, metric, k)
     np.testing.assert_array_equal(fr, sr)
@@ -558,12 +555,9 @@ def test_batched_filter_extreme_rows_and_queries(eng, metric):
     q[2] = xh[big[0]]                      # a query out of fp16 range
     q[3] = xh[big[12]]                     # a tiny query
     q[4] = 0.0
-    for image in ("1", "0"):
-        os.environ["FENIX_AMD_FILTER_IMAGE"] = image
-        try:
+    for image in (8, 16, 0):
+        with _lib.options(filter_image=image):
             fd, fr = gpu_search(eng, x, q, metric, k)
-        finally:
-            del os.environ["FENIX_AMD_FILTER_IMAGE"]
         with _lib.options(batched=0):
             sd, sr = gpu_search(eng, x, q, metric, k)
         np.testing.assert_array_equal(fr, sr)
@@ -728,10 +722,10 @@ def test_filter_image8_contents(eng):
 @pytest.mark.parametrize("metric", METRICS)
 @pytest.mark.parametrize("n,d,nq,k", [(100_000, 768, 40, 100), (60_000, 256, 256, 64),
                                       (30_000, 64, 2, 300), (20_000, 136, 70, 25)])
-def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k, bits):
+def test_filter_image_bit_identical(eng, metric, n, d, nq, k, bits):
     """Batched f32 searches through the int8 (the default) and the fp16
     filter images equal the same searches without one
-    (FENIX_AMD_FILTER_IMAGE=0) and the single-query scan, bit for bit, over
+    (option filter_image=0) and the single-query scan, bit for bit, over
     rows the images cannot represent (beyond fp16 range, infinities, NaN,
     subnormal, zero)."""
     xh = _extreme_rows(n, d, 43)
@@ -739,7 +733,6 @@ def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k, bits)
     q = O.fill_normal(nq, d, seed=44)
     q[0] *= 2.0 ** 50
     q[min(1, nq - 1)] = xh[7] if nq > 1 else q[0]
-    monkeypatch.delenv("FENIX_AMD_FILTER_IMAGE", raising=False)
     eng.clear_images()
     with _lib.options(filter_image=bits):
         # (int8 images serve k <= 256: capi.hip kI8MaxK)
@@ -751,8 +744,8 @@ def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k, bits)
     else:
         assert id(x) not in eng._images
     eng.clear_images()
-    monkeypatch.setenv("FENIX_AMD_FILTER_IMAGE", "0")
-    nd, nr = gpu_search(eng, x, q, metric, k)
+    with _lib.options(filter_image=0):
+        nd, nr = gpu_search(eng, x, q, metric, k)
     with _lib.options(batched=0):
         sd, sr = gpu_search(eng, x, q, metric, k)
     for dd, rr in ((id_, ir), (nd, nr)):
@@ -762,7 +755,7 @@ def test_filter_image_bit_identical(eng, monkeypatch, metric, n, d, nq, k, bits)
 
 @pytest.mark.parametrize("bits", [8, 16])
 @pytest.mark.parametrize("metric", METRICS)
-def test_single_query_through_filter_image(eng, monkeypatch, metric, bits):
+def test_single_query_through_filter_image(eng, metric, bits):
     """"batch_min_queries" = 1: single queries take the batched filter over
     the image (64-query tiles, one live query) and still equal the scan bit
     for bit, also through the overflow fallback ("force_fallback": the
@@ -772,7 +765,6 @@ def test_single_query_through_filter_image(eng, monkeypatch, metric, bits):
     n, d, k = 80_000, 256, 100
     xh = _extreme_rows(n, d, 45)
     x = torch.from_numpy(xh).to(eng.device)
-    monkeypatch.delenv("FENIX_AMD_FILTER_IMAGE", raising=False)
     eng.clear_images()
     with _lib.options(batch_min_queries=1, filter_image=bits):
         assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, 1, k, _lib.METRICS[metric])
@@ -804,12 +796,11 @@ def test_single_query_through_filter_image(eng, monkeypatch, metric, bits):
         assert not _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, k, m)
 
 
-def test_filter_image_follows_corpus_changes(eng, monkeypatch):
+def test_filter_image_follows_corpus_changes(eng):
     """The cached image is keyed on the corpus tensor's version: an in-place
     torch update and a rewrite through Engine.fill both rebuild it, so the
     batched results keep equalling the scan's."""
     n, d, nq, k = 50_000, 128, 32, 20
-    monkeypatch.delenv("FENIX_AMD_FILTER_IMAGE", raising=False)
     x = gpu_fill(eng, n, d, seed=51)
     q = O.fill_normal(nq, d, seed=52)
     gpu_search(eng, x, q, "l2", k)

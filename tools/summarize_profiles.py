@@ -38,6 +38,9 @@ def main() -> None:
     p.add_argument("--tag", default="")
     p.add_argument("--per-search", type=int, default=1,
                    help="matching launches per search (summed): the filter's phases")
+    p.add_argument("--searches", type=int, default=0,
+                   help="searches the run made: FETCH_SIZE of every matching launch summed "
+                        "and divided by it (instead of --per-search)")
     p.add_argument("--library-sha", default=None,
                    help="SHA-256 prefix of the library the pass ran (default: hash the "
                         "in-tree fenix_amd/lib/libfenix_knn.so, which must be that build)")
@@ -48,14 +51,24 @@ def main() -> None:
     pre = f"r{a.round:02d}{a.tag}"
     if a.stats:
         shutil.copy(a.stats, os.path.join(out_dir, f"{pre}_kernel_stats.csv"))
+        # the named kernel's average launch, from the same summary
+        for r in csv.DictReader(open(a.stats)):
+            if a.kernel in r.get("Name", r.get("KernelName", "")):
+                print(json.dumps({"kernel": r.get("Name"), "calls": r.get("Calls"),
+                                  "average_ns": r.get("AverageNs")}))
     if a.pmc:
         vals = collections.defaultdict(list)
         for r in csv.DictReader(open(a.pmc)):
             if a.kernel in r["Kernel_Name"]:
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
         fetch = vals.get("FETCH_SIZE", [])
-        searches = len(fetch) // a.per_search
-        mean_kib = sum(fetch[: searches * a.per_search]) / searches
+        if a.searches:
+            searches = a.searches
+            mean_kib = sum(fetch) / searches
+            a.per_search = len(fetch) / searches
+        else:
+            searches = len(fetch) // a.per_search
+            mean_kib = sum(fetch[: searches * a.per_search]) / searches
         hbm = mean_kib * 1024 * 2
         if a.library_sha is None:
             import sys
