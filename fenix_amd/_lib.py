@@ -58,6 +58,9 @@ SYMBOLS = (
     "fx_knn_search_img8",
     "fx_knn_reduce_img8",
     "fx_filter_image8_typed",
+    "fx_filter_image8_perm",
+    "fx_knn_filter_counts",
+    "fx_knn_filter_state",
     "fx_knn_distances",
     "fx_topk_merge_workspace_bytes",
     "fx_topk_merge",
@@ -162,6 +165,14 @@ def load() -> ctypes.CDLL:
         L.fx_filter_image8.restype = ci
         L.fx_filter_image8_typed.argtypes = [vp, ci, i64, i64, vp, vp, vp]
         L.fx_filter_image8_typed.restype = ci
+        L.fx_filter_image8_perm.argtypes = [i64, ctypes.POINTER(ctypes.c_uint64)]
+        L.fx_filter_image8_perm.restype = ci
+        L.fx_knn_filter_counts.argtypes = [vp, ci, i64, i64, i64, ci, i64, ci, vp, sz, vp,
+                                           ctypes.POINTER(i64), vp]
+        L.fx_knn_filter_counts.restype = ci
+        L.fx_knn_filter_state.argtypes = [vp, ci, i64, i64, i64, ci, i64, ci, vp, sz, vp, vp, vp,
+                                          vp]
+        L.fx_knn_filter_state.restype = ci
         L.fx_knn_scan_img8.argtypes = L.fx_knn_scan_img.argtypes
         L.fx_knn_scan_img8.restype = ci
         L.fx_knn_search_img8.argtypes = L.fx_knn_search_img.argtypes
@@ -254,6 +265,13 @@ def filter_image_used(n: int, d: int, dtype: int, nq: int, k: int, metric: int) 
     out = ctypes.c_int(0)
     check(load().fx_filter_image_used(n, d, dtype, nq, k, metric, ctypes.byref(out)))
     return bool(out.value)
+
+
+def image8_perm(n: int) -> int:
+    """fx_filter_image8_perm: int8 image row i holds corpus row (mult * i) % n."""
+    out = ctypes.c_uint64(0)
+    check(load().fx_filter_image8_perm(n, ctypes.byref(out)))
+    return int(out.value)
 
 
 def merge_workspace_bytes(nq: int, parts: int, kin: int, k: int) -> int:

@@ -554,6 +554,132 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
                         metric, thr, st);
 }
 
+// The int8 image's phases (fx_filter_image8; rows in image8_perm order, so
+// every sample is equidistributed over the corpus):
+//   sampling phases 0 .. m-3: phase 0 appends every pair of its <= cap rows,
+//     later ones the upper bounds at or below the previous threshold; the k-th
+//     upper bound is the next threshold, and after phase m-3 the exact
+//     distances of the k best upper bounds (launch_exact_kth) set it;
+//   F1 (phase m-2, the last sample's tiles): every pair whose lower bound
+//     reaches that threshold, appended with both bounds into the final
+//     candidate buffer; the exact k-th of its k best upper bounds is the
+//     next, much tighter threshold;
+//   overflow gate: F1's candidates under the new threshold, scaled to the
+//     tiles left, predict the final count; a query predicted past cap skips
+//     the final pass and goes to the exact scan (fx_knn_reduce's fallback);
+//   F2 (phase m-1): every tile F1 did not read, lower bound against the new
+//     threshold, appended after F1's candidates.  Each image row is read
+//     once by F1 or F2 (the sampling phases re-read 1/r^2 + ... of them);
+//   the exact k-th of all candidates' k best upper bounds is the final
+//     threshold, and the candidates whose lower bound reaches it are
+//     rescored exactly (launch_rescore), fx_knn_reduce selects the top k.
+static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, const void* image,
+                            const float* rowinfo, int64_t n, int64_t d, int64_t row_base,
+                            const float* Q, int64_t nq, int metric, int64_t k,
+                            const uint32_t* mask, char* w, hipStream_t st) {
+  float* qnorm = reinterpret_cast<float*>(w + b.off_qnorm);
+  uint64_t* thr = reinterpret_cast<uint64_t*>(w + b.off_thr);
+  uint32_t* count = reinterpret_cast<uint32_t*>(w + b.off_count);
+  uint64_t* cand = reinterpret_cast<uint64_t*>(w + b.off_cand);
+  uint64_t* cand_ub = reinterpret_cast<uint64_t*>(w + b.off_cand_ub);
+  float* topd = reinterpret_cast<float*>(w + b.off_topd);
+  int64_t* topr = reinterpret_cast<int64_t*>(w + b.off_topr);
+  const int64_t nq_pad8 = (nq + 255) / 256 * 256;
+  int rc = launch_qprep8(Q, nq, nq_pad8, (int)d, b.dq, metric,
+                         reinterpret_cast<int8_t*>(w + b.off_qh),
+                         reinterpret_cast<float*>(w + b.off_qinfo), st);
+  if (rc) return rc;
+  if (metric == FX_METRIC_COS) {  // the scan's max(|q|, 1e-12) for the exact distances
+    rc = launch_qnorm(Q, nq, (int)d, qnorm, st, 0);
+    if (rc) return rc;
+  }
+  const size_t count_bytes = (size_t)nq * 4 * kCountStride;
+  hipError_t e = hipMemsetAsync(thr, 0xFF, (size_t)nq * 8, st);
+  if (e == hipSuccess) e = hipMemsetAsync(count, 0, count_bytes, st);
+  if (e != hipSuccess) {
+    set_error("batched memset: %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  const bool merge_zeroes = b.merge.levels == 1;
+  auto args = [&](int ph) {
+    FilterArgs a = {};
+    a.X = image;
+    a.dtype = FX_DTYPE_F16;
+    a.rowinfo = rowinfo;
+    a.n = n;
+    a.d = (int)d;
+    a.row_base = row_base;
+    a.Qh = reinterpret_cast<const uint16_t*>(w + b.off_qh);
+    a.dq = b.dq;
+    a.qstride = nq_pad8;
+    a.img8 = 1;
+    a.perm_a = image8_perm(n);
+    a.qinfo = reinterpret_cast<const float*>(w + b.off_qinfo);
+    a.nq = nq;
+    a.mask = mask;
+    a.tile_start = b.start[ph];
+    a.tile_stride = b.stride[ph];
+    a.num_tiles = b.num[ph];
+    a.thr = thr;
+    a.count = count;
+    a.cand = cand;
+    a.cap = (int)b.cap;
+    a.diag = diag_env("FX_FILTER_DIAG", 0);
+    return a;
+  };
+  // the exact k-th of the k best upper bounds in `keys` -> thr
+  auto exact_threshold = [&](const uint64_t* keys, bool zero) {
+    int r = run_merge(b.merge, keys, nq, k, w + b.off_merge, topd, topr, st, nullptr, nullptr, 0,
+                      count, zero);
+    if (r) return r;
+    return launch_exact_kth(X, dtype, n, (int)d, row_base, Q, qnorm, nq, (int)k, topr, metric,
+                            thr, st);
+  };
+  const int m = b.nphases;
+  for (int ph = 0; ph + 2 < m; ++ph) {  // sampling phases: thresholds only
+    FilterArgs a = args(ph);
+    a.all_pass = ph == 0 ? 1 : 0;
+    a.ub_test = ph > 0 && option(kOptBatchUbTest) != 0 ? 1 : 0;
+    rc = launch_filter(a, metric, st);
+    if (rc) return rc;
+    rc = ph + 3 == m ? exact_threshold(cand, true)
+                     : run_merge(b.merge, cand, nq, k, w + b.off_merge, nullptr, nullptr, st, thr,
+                                 nullptr, 0, count, true);
+    if (rc) return rc;
+    if (!merge_zeroes && (e = hipMemsetAsync(count, 0, count_bytes, st)) != hipSuccess) {
+      set_error("batched memset: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+  }
+  // F1: the last sample's tiles (with one phase: every tile), both bounds
+  FilterArgs f1 = args(m >= 2 ? m - 2 : 0);
+  f1.all_pass = m <= 2 ? 1 : 0;
+  f1.cand_ub = cand_ub;
+  rc = launch_filter(f1, metric, st);
+  if (rc) return rc;
+  if (m >= 2) {
+    rc = exact_threshold(cand_ub, false);
+    if (rc) return rc;
+    const int64_t t1 = b.num[m - 2], t2 = b.tiles - t1;
+    if (t2 > 0) {
+      rc = launch_overflow_gate(cand, count, thr, nq, (int)b.cap, t2, t1, st);
+      if (rc) return rc;
+      // F2: the tiles F1 did not read (plan tile p -> p + p / (r - 1) + 1)
+      FilterArgs f2 = args(m - 1);
+      f2.num_tiles = t2;
+      f2.tile_skip = b.stride[m - 2];
+      f2.cand_ub = cand_ub;
+      f2.skip_full = 1;
+      rc = launch_filter(f2, metric, st);
+      if (rc) return rc;
+    }
+  }
+  rc = exact_threshold(cand_ub, false);
+  if (rc) return rc;
+  return launch_rescore(X, dtype, n, (int)d, row_base, Q, qnorm, nq, count, cand, (int)b.cap,
+                        metric, thr, st);
+}
+
 #ifdef FX_DIAG_BUILD
 static int batched_phases(const BatchLayout& b, const float* X, int64_t n, int64_t d,
                           int64_t row_base, const float* Q, int64_t nq, int metric, int64_t k,
@@ -617,7 +743,7 @@ using namespace fx;
 
 extern "C" {
 
-int fx_version(void) { return 103; }
+int fx_version(void) { return 104; }
 
 const char* fx_last_error(void) { return g_err; }
 
@@ -750,8 +876,8 @@ static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_
         if (v >= 2) r = v < rmax ? v : rmax;
         rc = plan_phases(&b, filter_tile_rows(dtype), r);
         if (rc) return rc;
-        return filter_phases(b, corpus, dtype, image, rowinfo, true, n, d, row_base, queries, nq,
-                             metric, k, mask, reinterpret_cast<char*>(ws), st);
+        return filter_phases_i8(b, corpus, dtype, image, rowinfo, n, d, row_base, queries, nq,
+                                metric, k, mask, reinterpret_cast<char*>(ws), st);
       }
       return filter_phases(s.batch, corpus, dtype, img ? image : nullptr, rowinfo, false, n, d,
                            row_base, queries, nq, metric, k, mask, reinterpret_cast<char*>(ws),
@@ -873,6 +999,15 @@ int fx_filter_image8_bytes(int64_t n, int64_t d, size_t* image_bytes, size_t* ro
   return FX_OK;
 }
 
+int fx_filter_image8_perm(int64_t n, uint64_t* mult) {
+  if (!mult || n < 0) {
+    set_error("fx_filter_image8_perm: n=%lld", (long long)n);
+    return FX_EINVAL;
+  }
+  *mult = image8_perm(n);
+  return FX_OK;
+}
+
 int fx_filter_image8(const float* corpus, int64_t n, int64_t d, void* image, float* rowinfo,
                      void* stream) {
   return fx_filter_image8_typed(corpus, FX_DTYPE_F32, n, d, image, rowinfo, stream);
@@ -960,6 +1095,61 @@ static int reduce_impl(const void* corpus, int dtype, int64_t n, int64_t d, int6
   return fallback_search(s, corpus, dtype, n, d, row_base, queries, nq, metric, k, mask,
                          reinterpret_cast<const uint32_t*>(w + b.off_count), gate_cap,
                          w + s.single_off, out_dist, out_row, st);
+}
+
+int fx_knn_filter_state(const void* corpus, int dtype, int64_t n, int64_t d, int64_t nq,
+                        int metric, int64_t k, int img8, const void* ws, size_t ws_bytes,
+                        uint64_t* out_thr, uint64_t* out_cand, uint64_t* out_cand_ub,
+                        void* stream) {
+  SearchLayout s;
+  int rc = search_layout(corpus, dtype, n, d, nq, metric, k, const_cast<void*>(ws), ws_bytes, &s,
+                         img8 != 0);
+  if (rc) return rc;
+  if (!s.batched || !s.batch.filter) {
+    set_error("fx_knn_filter_state: the search did not run the filter");
+    return FX_EINVAL;
+  }
+  const char* w = reinterpret_cast<const char*>(ws);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const size_t cb = (size_t)nq * s.batch.cap * 8;
+  hipError_t e = hipSuccess;
+  if (out_thr) e = hipMemcpyAsync(out_thr, w + s.batch.off_thr, (size_t)nq * 8,
+                                  hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess && out_cand)
+    e = hipMemcpyAsync(out_cand, w + s.batch.off_cand, cb, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess && out_cand_ub)
+    e = hipMemcpyAsync(out_cand_ub, w + s.batch.off_cand_ub, cb, hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) {
+    set_error("fx_knn_filter_state: %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  return FX_OK;
+}
+
+int fx_knn_filter_counts(const void* corpus, int dtype, int64_t n, int64_t d, int64_t nq,
+                         int metric, int64_t k, int img8, const void* ws, size_t ws_bytes,
+                         uint32_t* out_counts, int64_t* out_cap, void* stream) {
+  SearchLayout s;
+  int rc = search_layout(corpus, dtype, n, d, nq, metric, k, const_cast<void*>(ws), ws_bytes, &s,
+                         img8 != 0);
+  if (rc) return rc;
+  if (!out_counts || !out_cap) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  if (!s.batched) {
+    *out_cap = -1;
+    return FX_OK;
+  }
+  *out_cap = s.batch.cap;
+  const char* c = reinterpret_cast<const char*>(ws) + s.batch.off_count;
+  hipError_t e = hipMemcpy2DAsync(out_counts, 4, c, 4 * kCountStride, 4, (size_t)nq,
+                                  hipMemcpyDeviceToDevice, reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) {
+    set_error("fx_knn_filter_counts: %s", hipGetErrorString(e));
+    return FX_EHIP;
+  }
+  return FX_OK;
 }
 
 int fx_knn_reduce(const void* corpus, int dtype, int64_t n, int64_t d, int64_t row_base,

@@ -167,6 +167,10 @@ struct FilterArgs {
                           // launch_qprep8
   int all_pass;           // no query has a threshold yet (thr all empty): img8 appends
                           // every live pair without the test
+  int64_t tile_skip;      // > 1: the plan's tiles skip every tile_skip-th tile (img8 final
+                          // pass: the last sample's tiles were read with its threshold)
+  int skip_full;          // a workgroup whose queries all hold count > cap returns at once
+  uint64_t perm_a;        // img8: image row i holds corpus row (perm_a * i) % n (image8_perm)
   int ub_test;            // sampling phase after the first: append when the UPPER bound
                           // reaches the threshold (only the k-th upper bound is needed)
   int diag;               // FX_FILTER_DIAG (diagnostic builds only): 1 no appends, 2 no epilogue,
@@ -189,6 +193,24 @@ constexpr int kI8QInfo = 4;
 constexpr float kI8Kappa = 128.f;
 int launch_image8(const void* X, int dtype, int64_t n, int d, void* img, float* rowinfo,
                   hipStream_t stream);
+// The int8 image stores its rows in the order of an affine permutation of the
+// corpus: image row i holds corpus row (a * i) % n, a ~ 0.618 n coprime with n
+// (a Weyl sequence).  The filter's nested samples take every r-th tile of the
+// IMAGE, so they are equidistributed over the corpus whatever its order: a
+// corpus stored in clusters (the reference test's x + 10 x0 per 1 000-row
+// batch) or sorted by any key no longer hides its nearest rows from the
+// samples.  1 for n <= 2.
+uint64_t image8_perm(int64_t n);
+__device__ __forceinline__ uint32_t perm_row(uint64_t a, int64_t n, int64_t i) {
+  return (uint32_t)((a * (uint64_t)i) % (uint64_t)n);
+}
+// Final-pass overflow prediction (img8): per query, the appended candidates of
+// the last sample (count, cand: lb composites) that pass the new threshold thr,
+// scaled by num / den (the remaining tiles over the sample's), plus count: a
+// query predicted to exceed cap gets count = cap + 1 (the final pass skips it
+// and the exact scan recomputes it, fx_knn_reduce's gated fallback)
+int launch_overflow_gate(const uint64_t* cand, uint32_t* count, const uint64_t* thr, int64_t nq,
+                         int cap, int64_t num, int64_t den, hipStream_t stream);
 int launch_qprep8(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
                   int8_t* Qb, float* qinfo, hipStream_t stream);
 int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,

@@ -1203,6 +1203,7 @@ struct Img3Shared {
   uint32_t segbase[fBQ];
   float rext[kI3BM];  // int8 image: 1 / s of the row
   f32x4 qinf[fBQ];   // int8 image: the query's launch_qprep8 record
+  uint32_t rrow[kI3BM];  // int8 image: the global corpus row of the tile row (image8_perm)
 };
 static_assert(sizeof(Img3Shared) * (fWaves / kI3Waves) <= 160 * 1024,
               "filter_img3_kernel: LDS over 160 KB per CU");
@@ -1474,10 +1475,10 @@ __device__ __forceinline__ void i8_note_row(float* rinfo, float* rterm, float* r
 template <int METRIC>
 __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const float* rinfo,
                                             const float* rterm, const float* rext,
-                                            const uint32_t* flags, const f32x4* qtab,
-                                            const f32x4* qinf, const FilterArgs& a, int64_t q0,
-                                            int64_t r0, int wid, int h, int l32, uint32_t* seg,
-                                            int diag) {
+                                            const uint32_t* rrow, const uint32_t* flags,
+                                            const f32x4* qtab, const f32x4* qinf,
+                                            const FilterArgs& a, int64_t q0, int wid, int h,
+                                            int l32, uint32_t* seg, int diag) {
   constexpr int SEG = FX_I3_SEG;
   const int lr0 = wid * 32 + 4 * h;
   const uint32_t fmask = flags[wid * 2 + h], smask = flags[16 + wid * 2 + h];
@@ -1517,9 +1518,12 @@ __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const fl
     }
   }
   uint32_t pm[kI2QT];
+  // (all_pass: every live row, whatever the test says: with R' = inf a zero
+  // row's 0 * inf is a NaN whose sign decides the bit)
+  const uint32_t force = a.all_pass ? ~0u : fmask;
 #pragma unroll
   for (int u = 0; u < kI2QT; ++u) {
-    pm[u] = (diag & 1) ? 0u : (~fail[u] | fmask) & ~smask & 0xffffu;
+    pm[u] = (diag & 1) ? 0u : (~fail[u] | force) & ~smask & 0xffffu;
     if (q0 + u * 32 + l32 >= a.nq) pm[u] = 0u;
   }
   if (a.all_pass) {  // no threshold yet (first phase): every live pair, slots reserved
@@ -1540,7 +1544,7 @@ __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const fl
         float lb, ub;
         i8_bounds<METRIC>(acc[u][jj], rinfo[lr], rterm[lr], rext[lr], qrec, a.d, lb, ub);
         if (p < (uint32_t)a.cap) {
-          const uint32_t grow = (uint32_t)(a.row_base + r0) + (uint32_t)lr;
+          const uint32_t grow = rrow[lr];
           const size_t slot = (size_t)gq * a.cap + p;
           if (a.cand_ub != nullptr) {
             a.cand[slot] = make_comp(lb, grow);
@@ -1587,7 +1591,7 @@ __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const fl
       const int lr = lr0 + (j & 3) + 8 * (j >> 2);
       float lb, ub;
       i8_bounds<METRIC>(x, rinfo[lr], rterm[lr], rext[lr], qrec, a.d, lb, ub);
-      const uint32_t grow = (uint32_t)(a.row_base + r0) + (uint32_t)lr;
+      const uint32_t grow = rrow[lr];
       if (p < (uint32_t)SEG) {
         uint32_t* e = seg + fBQ + 3 * (qi * SEG + p);
         e[0] = order_key(lb);
@@ -1635,10 +1639,21 @@ __global__ void __launch_bounds__(kI3Threads, 2) filter_img3_kernel(FilterArgs a
   const int64_t ntile32 = (a.n + 31) / 32;
   // workgroup tiles: kI3Sub per fBM-row tile of the plan (a.tile_start, ...)
   const int64_t ntiles = a.num_tiles * kI3Sub;
+  // (tile_skip > 1: plan tile p maps past every tile_skip-th tile, the ones
+  // the last sample read)
+  const int64_t skip1 = a.tile_skip > 1 ? a.tile_skip - 1 : 0;
   auto tile_r0 = [&](int64_t ti) {
-    return (a.tile_start + (ti / kI3Sub) * a.tile_stride) * fBM + (ti % kI3Sub) * kI3BM;
+    int64_t pt = a.tile_start + (ti / kI3Sub) * a.tile_stride;
+    if (skip1 > 0) pt += pt / skip1 + 1;
+    return pt * fBM + (ti % kI3Sub) * kI3BM;
   };
   if ((int64_t)blockIdx.x >= ntiles) return;
+  if (a.skip_full) {  // every query of the tile predicted to overflow: nothing to do
+    bool full = true;
+    for (int q = tid; q < fBQ; q += kI3Threads)
+      if (q0 + q < a.nq && a.count[(q0 + q) * kCountStride] <= (uint32_t)a.cap) full = false;
+    if (__syncthreads_and(full)) return;
+  }
   if constexpr (I8)
     i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, kI3Threads);
   else
@@ -1851,13 +1866,17 @@ __global__ void __launch_bounds__(kI3Threads, 2) filter_img3_kernel(FilterArgs a
           rsum = *reinterpret_cast<const f32x4*>(a.rowinfo + row * kI8RowInfo);
         else
           rsum = a.rowinfo[row];
+        // (int8 image: the mask bit of the corpus row the image row holds)
+        int64_t mrow = row;
+        if constexpr (I8) mrow = perm_row(a.perm_a, a.n, row);
         // (both kernel arguments: global loads; a pointer to a __device__
         // constant made a flat load, which counts in lgkmcnt too, and the
         // step's LDS waits then waited for it)
         const bool masked = a.mask != nullptr;
-        const uint32_t* mp = masked ? a.mask + (row >> 5)
+        const uint32_t* mp = masked ? a.mask + (mrow >> 5)
                                     : reinterpret_cast<const uint32_t*>(a.rowinfo) + row * (I8 ? kI8RowInfo : 1);
         mword = *mp | (masked ? 0u : ~0u);
+        if constexpr (I8) mword = masked ? (mword >> (mrow & 31)) << (row & 31) : mword;
       }
       compute(xa[S], rslot, std::bool_constant<decltype(first)::value && S == 0>{});
       rslot = rslot + 1 == kI3Slots ? 0 : rslot + 1;
@@ -1893,6 +1912,7 @@ __global__ void __launch_bounds__(kI3Threads, 2) filter_img3_kernel(FilterArgs a
       if constexpr (I8) {  // {omega, 1/s, N/s, n^2/s}
         const float y1 = METRIC == 1 ? rsum[1] : METRIC == 2 ? rsum[2] : rsum[3];
         i8_note_row(sh->rinfo, sh->rterm, sh->rext, sh->rflags[par], lr, rsum[0], y1, rsum[1], ok);
+        sh->rrow[lr] = (uint32_t)a.row_base + (row < a.n ? perm_row(a.perm_a, a.n, row) : 0u);
       } else {
       const float s = ok ? rsum : 0.f;
       float rv;
@@ -1912,8 +1932,8 @@ __global__ void __launch_bounds__(kI3Threads, 2) filter_img3_kernel(FilterArgs a
       if (acc[0][0] == 1.2345f) a.count[0] = 7;
     } else {
       if constexpr (I8)
-        i8_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rext, sh->rflags[par], sh->qtab,
-                            sh->qinf, a, q0, r0, wid, h, l32, sh->seg, diag);
+        i8_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rext, sh->rrow, sh->rflags[par],
+                            sh->qtab, sh->qinf, a, q0, wid, h, l32, sh->seg, diag);
       else
         i3_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rflags[par], sh->qtab, sh->qab, a, q0,
                             r0, wid, h, l32, sh->seg, diag);
@@ -3480,10 +3500,13 @@ typedef float img_f32x16 __attribute__((ext_vector_type(16)));
 // T: the corpus's value type, float or _Float16 (the values are the same
 // reals in f32, so the bounds below are unchanged; the candidates are rescored
 // from the T rows in the scan's order)
+// Image row r holds corpus row perm_row(pa, n, r) (image8_perm): the tile's
+// 32 rows come from 32 places of the corpus, each still read as whole
+// 128-B lines.
 template <typename T>
 __global__ void __launch_bounds__(256) image8_kernel(const T* __restrict__ X, int64_t n, int d,
                                                     int8_t* __restrict__ img,
-                                                    float* __restrict__ rowinfo) {
+                                                    float* __restrict__ rowinfo, uint64_t pa) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int64_t nt = (n + 31) / 32;
   const int ksteps = (d + 31) / 32;
@@ -3492,7 +3515,7 @@ __global__ void __launch_bounds__(256) image8_kernel(const T* __restrict__ X, in
   for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < nt; t += nw) {
     const int64_t r = t * 32 + (lane & 31);
     const bool live = r < n;
-    const T* xr = X + (live ? r : 0) * (int64_t)d;
+    const T* xr = X + (live ? (int64_t)perm_row(pa, n, r) : 0) * (int64_t)d;
     auto load = [&](int ks) {  // components 32 ks + 16 h .. + 15 (zeros past d)
       img_f32x16 v;
       const int k0 = 32 * ks + 16 * h;
@@ -3577,6 +3600,59 @@ __global__ void __launch_bounds__(256) image8_kernel(const T* __restrict__ X, in
   }
 }
 
+static uint64_t gcd64(uint64_t a, uint64_t b) {
+  while (b != 0) {
+    const uint64_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+uint64_t image8_perm(int64_t n) {
+  if (n <= 2) return 1;
+  uint64_t a = (uint64_t)((double)n * 0.6180339887498949) | 1u;
+  while (gcd64(a, (uint64_t)n) != 1) a += 2;
+  return a % (uint64_t)n;
+}
+
+// One workgroup per query (launch_overflow_gate, fx_internal.h)
+__global__ void __launch_bounds__(256) overflow_gate_kernel(const uint64_t* __restrict__ cand,
+                                                            uint32_t* __restrict__ count,
+                                                            const uint64_t* __restrict__ thr,
+                                                            int cap, int64_t num, int64_t den) {
+  const int64_t q = blockIdx.x;
+  __shared__ uint32_t tot;
+  const uint32_t c = count[q * kCountStride];
+  if (c > (uint32_t)cap) return;  // (already overflowing: recomputed anyway)
+  if (threadIdx.x == 0) tot = 0u;
+  __syncthreads();
+  const uint32_t t = (uint32_t)(thr[q] >> 32);
+  const uint64_t* cq = cand + q * (int64_t)cap;
+  uint32_t mine = 0u;
+  for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) mine += (uint32_t)(cq[i] >> 32) <= t;
+  for (int o = 32; o >= 1; o >>= 1) mine += __shfl_xor(mine, o);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&tot, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t predicted = (uint64_t)c + ((uint64_t)tot * (uint64_t)num + (uint64_t)den - 1) /
+                                                 (uint64_t)den;
+    if (predicted > (uint64_t)cap) count[q * kCountStride] = (uint32_t)cap + 1u;
+  }
+}
+
+int launch_overflow_gate(const uint64_t* cand, uint32_t* count, const uint64_t* thr, int64_t nq,
+                         int cap, int64_t num, int64_t den, hipStream_t stream) {
+  if (nq <= 0) return FX_OK;
+  if (nq > 0x7fffffffll || den <= 0) {
+    set_error("overflow gate: nq=%lld den=%lld", (long long)nq, (long long)den);
+    return FX_EINVAL;
+  }
+  hipLaunchKernelGGL(overflow_gate_kernel, dim3((unsigned)nq), dim3(256), 0, stream, cand, count,
+                     thr, cap, num, den);
+  return check_launch("overflow_gate_kernel");
+}
+
 int launch_image8(const void* X, int dtype, int64_t n, int d, void* img, float* rowinfo,
                   hipStream_t stream) {
   if (n <= 0) return FX_OK;
@@ -3585,14 +3661,15 @@ int launch_image8(const void* X, int dtype, int64_t n, int d, void* img, float* 
   if (rc) return rc;
   int64_t blocks = ((n + 31) / 32 + 3) / 4;
   if (blocks > (int64_t)cus * 8) blocks = (int64_t)cus * 8;
+  const uint64_t pa = image8_perm(n);
   if (dtype == FX_DTYPE_F16)
     hipLaunchKernelGGL(image8_kernel<_Float16>, dim3((unsigned)blocks), dim3(256), 0, stream,
                        reinterpret_cast<const _Float16*>(X), n, d, reinterpret_cast<int8_t*>(img),
-                       rowinfo);
+                       rowinfo, pa);
   else
     hipLaunchKernelGGL(image8_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, stream,
                        reinterpret_cast<const float*>(X), n, d, reinterpret_cast<int8_t*>(img),
-                       rowinfo);
+                       rowinfo, pa);
   return check_launch("image8_kernel");
 }
 

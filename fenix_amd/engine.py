@@ -619,6 +619,21 @@ class Engine:
             )
         )
 
+    def filter_counts(self, shard: Shard, nq: int, metric: int, k: int,
+                      state: "ScanState") -> Tuple[Optional[np.ndarray], int]:
+        """fx_knn_filter_counts after ``scan``: each query's final candidate
+        count (> cap: the exact scan recomputed it) and the capacity; (None,
+        -1) when the scan did not run the filter.  Synchronises (tests, tools)."""
+        out = torch.zeros(nq, dtype=torch.int32, device=self.device)
+        cap = ctypes.c_int64(0)
+        _lib.check(_lib.load().fx_knn_filter_counts(
+            _ptr(shard.data), shard.dtype_id, shard.n, shard.d, nq, metric, k,
+            1 if (state.bits == 8 and state.image is not None) else 0, _ptr(state.ws),
+            state.ws.numel(), _ptr(out), ctypes.byref(cap), self._stream()))
+        if cap.value < 0:
+            return None, -1
+        return out.cpu().numpy().view(np.uint32), int(cap.value)
+
     def merge(self, dist: torch.Tensor, row: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
         """fx_topk_merge of [nq, parts, kin] sorted lists -> [nq, k]."""
         nq, parts, kin = dist.shape

@@ -213,6 +213,27 @@ int fx_knn_search_img(const void* corpus, int dtype, int64_t n, int64_t d, int64
  * option is 8.
  */
 int fx_filter_image8_bytes(int64_t n, int64_t d, size_t* image_bytes, size_t* rowinfo_bytes);
+/* Row order of the int8 image: image row i (and rowinfo row i) holds corpus
+ * row (mult * i) % n, an affine permutation (mult ~ 0.618 n, coprime with n),
+ * so the filter's tile-strided samples are spread over the whole corpus even
+ * when it is stored in clusters or sorted.  For tests and tools. */
+int fx_filter_image8_perm(int64_t n, uint64_t* mult);
+/* After a batched / filter-image search (fx_knn_scan*, before the workspace
+ * is reused): each query's final candidate count (device uint32 [nq]) and
+ * the buffer's capacity (*out_cap; -1 when the search did not run the
+ * filter).  count > cap means the exact scan recomputed that query.  Same
+ * shape arguments as the scan; img8 = 1 when it received an int8 image.
+ * For tests and tools. */
+int fx_knn_filter_counts(const void* corpus, int dtype, int64_t n, int64_t d, int64_t nq,
+                         int metric, int64_t k, int img8, const void* ws, size_t ws_bytes,
+                         uint32_t* out_counts, int64_t* out_cap, void* stream);
+/* The same search's thresholds (device uint64 [nq] composites) and candidate
+ * buffers (device uint64 [nq][cap]: lower-bound / exact composites, upper-
+ * bound composites; each nullable).  For tests and tools. */
+int fx_knn_filter_state(const void* corpus, int dtype, int64_t n, int64_t d, int64_t nq,
+                        int metric, int64_t k, int img8, const void* ws, size_t ws_bytes,
+                        uint64_t* out_thr, uint64_t* out_cand, uint64_t* out_cand_ub,
+                        void* stream);
 int fx_filter_image8(const float* corpus, int64_t n, int64_t d, void* image, float* rowinfo,
                      void* stream);
 /* The same image of a float32 or float16 corpus (dtype FX_DTYPE_F32 /

@@ -40,7 +40,9 @@ def test_library_is_gfx950():
 
 def test_version_and_limits():
     lib = _lib.load()
-    assert lib.fx_version() == 103  # 1.3: int8 filter images (1.2: options, device-gated fallback)
+    # 1.4: int8 images in permuted row order (1.3: int8 filter images; 1.2:
+    # options, device-gated fallback)
+    assert lib.fx_version() == 104
     assert _lib.max_k() == 1024
 
 
@@ -120,3 +122,30 @@ def test_comm_argument_checks_without_gpu():
     assert b"twice" in L.fx_last_error()
     assert L.fx_comm_init_all(0, two, ctypes.byref(h)) == -1
     assert L.fx_comm_destroy(None) == 0
+
+
+def test_image8_row_permutation_is_a_bijection():
+    """fx_filter_image8_perm: image row i holds corpus row (mult * i) % n, a
+    bijection for every n (mult coprime with n), spreading consecutive corpus
+    rows: a 1 000-row cluster lands in ~1/8 of a stride-8 tile sample."""
+    import math
+
+    import numpy as np
+
+    for n in (0, 1, 2, 3, 7, 256, 1000, 65_537, 400_000, 1_000_003, 6_250_000):
+        a = _lib.image8_perm(n)
+        if n <= 2:
+            assert a == 1
+            continue
+        assert math.gcd(a, n) == 1 and 0 < a < n
+        if n <= 1_000_003:
+            rows = (a * np.arange(n, dtype=np.uint64)) % np.uint64(n)
+            assert len(np.unique(rows)) == n
+    n = 1_000_003
+    a = _lib.image8_perm(n)
+    i = np.arange(n, dtype=np.int64)
+    sample = ((a * i) % n)[(i // 256) % 8 == 0]
+    per_cluster = np.bincount(sample // 1000)[:-1]
+    assert per_cluster.min() >= 100 and per_cluster.max() <= 150  # expect 125
+    with pytest.raises(ValueError):
+        _lib.check(_lib.load().fx_filter_image8_perm(-1, ctypes.byref(ctypes.c_uint64())))

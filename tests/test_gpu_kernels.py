@@ -560,7 +560,8 @@ def test_batched_filter_extreme_rows_and_queries(eng, metric):
             fd, fr = gpu_search(eng, x, q, metric, k)
         with _lib.options(batched=0):
             sd, sr = gpu_search(eng, x, q, metric, k)
-        np.testing.assert_array_equal(fr, sr)
+        bad = np.nonzero((fr != sr).any(axis=1))[0]
+        np.testing.assert_array_equal(fr, sr, err_msg=f"image {image}: queries {bad}")
         np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32))
 
 
@@ -675,7 +676,8 @@ def _build_image8(x, n, d):
 
 def test_filter_image8_contents(eng):
     """fx_filter_image8: rows in the int8 MFMA-fragment layout [tile][k-step]
-    [lane half][row in tile][16]; per row x~ = rint(x / s) with |x~| <= 127,
+    [lane half][row in tile][16], in the permuted row order
+    (fx_filter_image8_perm); per row x~ = rint(x / s) with |x~| <= 127,
     |x~| <= 2048, every component within s/2 of x / s, and the bound terms
     {omega, 1/s, N/s, n^2/s}: omega >= |x~| + kappa |x - s x~| / s (float64
     reference), NaN exactly for non-finite rows, 0 for zero rows."""
@@ -687,8 +689,13 @@ def test_filter_image8_contents(eng):
     t, ks = (n + 31) // 32, (d + 31) // 32
     full = h.reshape(t, ks, 2, 32, 16).transpose(0, 3, 1, 2, 4).reshape(t * 32, ks * 32)
     assert not full[n:].any() and not full[:, d:].any(), "image padding is not zero"
-    xq = full[:n, :d].astype(np.float64)
-    inf = info.cpu().numpy().astype(np.float64)
+    # image row i holds corpus row (mult * i) % n (fx_filter_image8_perm):
+    # back to corpus order
+    perm = (_lib.image8_perm(n) * np.arange(n, dtype=np.int64)) % n
+    xq = np.empty((n, d))
+    xq[perm] = full[:n, :d].astype(np.float64)
+    inf = np.empty((n, 4))
+    inf[perm] = info.cpu().numpy().astype(np.float64)
     om, is_, nos, n2s = inf.T
     with np.errstate(over="ignore", invalid="ignore"):
         forced = ~np.isfinite(xh).all(axis=1)
