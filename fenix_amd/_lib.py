@@ -92,7 +92,8 @@ SYMBOLS = (
 # "batched", "batch_min_queries" and "filter_image" are user switches, the rest
 # test switches
 OPTIONS = ("batched", "batch_min_queries", "batch_cap", "batch_sample_ratio", "force_fallback",
-           "scan_interleave", "q8_dma", "filter_image", "batch_ub_test", "single_query_image")
+           "scan_interleave", "q8_dma", "filter_image", "batch_ub_test", "single_query_image",
+           "i8_max_k")
 
 _lock = threading.Lock()
 _lib = None

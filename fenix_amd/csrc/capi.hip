@@ -41,8 +41,9 @@ static std::mutex g_mu;
 static const char* const kOptNames[kOptCount] = {
     "batched", "batch_min_queries", "batch_cap", "batch_sample_ratio",
     "force_fallback", "scan_interleave", "q8_dma", "filter_image", "batch_ub_test",
-    "single_query_image"};
-static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}, {8}, {1}, {1}};
+    "single_query_image", "i8_max_k"};
+static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}, {8}, {1}, {1},
+                                                 {256}};
 
 int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
 
@@ -190,13 +191,16 @@ static constexpr int64_t kLargeMaxK = 0x7fffffffll;
 // A query whose final candidates overflow `cap` is recomputed exactly by the
 // single-query scan, gated on the device (fx_knn_reduce: no host sync).
 static constexpr int64_t kListLen = 4096;  // candidate buffer viewed as lists
-// sample growth per phase with an int8 filter image (filter_phases)
+// int8 filter image (filter_phases_i8): the final pass's sample F1 takes
+// every kI8SampleRatio-th tile, the samples before it grow by kI8GrowRatio
 static constexpr int64_t kI8SampleRatio = 8;
+static constexpr int64_t kI8GrowRatio = 16;
 
 struct BatchLayout {
   int64_t cap = 0, tiles = 0, nq_pad = 0;
   int nphases = 0;
   bool filter = false;  // fp16-MFMA filter + exact rescoring (knn_filter.hip)
+  bool img8 = false;    // planned for an int8 filter image (filter_phases_i8)
   int dq = 0;
   int64_t start[16], stride[16], num[16];
   MergePlan merge;
@@ -216,8 +220,8 @@ static constexpr int64_t kSingleImageMinBytes = (int64_t)4 << 30;
 // The int8 image's bounds are wide: with k = 1 000 the final phase of a
 // 6.25M x 1536 fp16 IP search appended more than its 64 K candidate slots for
 // most queries (Flight, profiles/r03_f16_int8_image.log), and each overflow
-// costs a full rescan.  Int8 images serve k <= kI8MaxK only.
-static constexpr int64_t kI8MaxK = 256;
+// costs a full rescan.  Int8 images serve k <= option "i8_max_k" only.
+static int64_t i8_max_k() { return option(kOptI8MaxK); }
 
 static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool aligned, int64_t n,
                         bool img8, int64_t k) {
@@ -225,7 +229,7 @@ static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool align
   // 2 queries: 6.5 ms vs 2 x 4.5 ms (10Mx768); "batch_min_queries" = 1 also
   // sends every single query through the filter
   int64_t min_q = option(kOptBatchMinQ) >= 1 ? option(kOptBatchMinQ) : 2;
-  if (nq == 1 && img8 && k <= kI8MaxK && option(kOptSingleImage) != 0 && d % 8 == 0 &&
+  if (nq == 1 && img8 && k <= i8_max_k() && option(kOptSingleImage) != 0 && d % 8 == 0 &&
       n * d * (dtype == FX_DTYPE_F32 ? 4 : 2) >= kSingleImageMinBytes)
     min_q = 1;
   if (!use_filter()) min_q = 8;  // the fp32-MFMA kernel breaks even with scans at ~8 queries
@@ -238,10 +242,18 @@ static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool align
 
 static int plan_phases(BatchLayout* b, int64_t tr, int64_t r);
 
-static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, BatchLayout* b) {
+static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, BatchLayout* b,
+                        bool img8) {
   b->filter = use_filter();
+  b->img8 = img8 && b->filter;
   const int64_t tr = b->filter ? filter_tile_rows(dtype) : batch_tile_rows();
   b->cap = 64 * k > 16384 ? 64 * k : 16384;
+  // int8 images: 4x the buffer.  Their bounds keep whole clusters of a
+  // clustered corpus against a generic query (10M x 768, x + 10 x0 per
+  // 1 000 rows, 256 cosine queries: median 10 K, largest 33 K candidates);
+  // every consumer reads only the count it was given (select_kernel streams
+  // any count), so the larger buffer costs memory, not time
+  if (b->img8) b->cap *= 4;
   if (option(kOptBatchCap) >= 16 * k) b->cap = option(kOptBatchCap);  // test: small buffers
   b->cap = (b->cap + kListLen - 1) / kListLen * kListLen;
   b->tiles = (n + tr - 1) / tr;
@@ -292,6 +304,35 @@ static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, 
 // Nested row samples of the batched phases: phase i scans every stride_i-th
 // tile of tr rows, each stride a multiple r of the next, the first at most
 // cap rows, the last every tile.
+// The int8 image's plan (filter_phases_i8): the last sample takes every
+// r1-th tile (F1, its complement is F2), the ones before it grow by r2
+// (their appends stay far below cap: about r2 k upper bounds per query),
+// the first holds at most cap rows.  10M x 768, r1 = 8, r2 = 16: 20, 306,
+// 4 883 tiles + the 34 180 F2 reads.
+static int plan_phases_i8(BatchLayout* b, int64_t tr, int64_t r1, int64_t r2) {
+  int64_t strides[16];
+  int m = 0;
+  strides[m++] = 1;
+  int64_t r = r1;
+  while ((b->tiles + strides[m - 1] - 1) / strides[m - 1] * tr > b->cap) {
+    if (m >= 15) {
+      set_error("batched sampling plan too deep");
+      return FX_EUNSUPPORTED;
+    }
+    strides[m] = strides[m - 1] * r;
+    ++m;
+    r = r2;
+  }
+  b->nphases = m;
+  for (int i = 0; i < m; ++i) {
+    const int64_t st = strides[m - 1 - i];
+    b->stride[i] = st;
+    b->start[i] = 0;
+    b->num[i] = (b->tiles + st - 1) / st;
+  }
+  return FX_OK;
+}
+
 static int plan_phases(BatchLayout* b, int64_t tr, int64_t r) {
   int64_t strides[16];
   int m = 0;
@@ -399,7 +440,9 @@ static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, i
   int rc = plan_fallback(n, d, dtype, nq, k, metric, aligned, s, &fq);
   if (rc) return rc;
   const size_t single_total = s->total;
-  rc = plan_batched(n, d, dtype, nq, k, &s->batch);
+  rc = plan_batched(n, d, dtype, nq, k, &s->batch,
+                    img8 && k <= i8_max_k() && d % 8 == 0 &&
+                        (dtype == FX_DTYPE_F32 || dtype == FX_DTYPE_F16));
   if (rc) return rc;
   s->batched = true;
   s->fb_queries = fq;
@@ -582,25 +625,16 @@ static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, cons
   uint32_t* count = reinterpret_cast<uint32_t*>(w + b.off_count);
   uint64_t* cand = reinterpret_cast<uint64_t*>(w + b.off_cand);
   uint64_t* cand_ub = reinterpret_cast<uint64_t*>(w + b.off_cand_ub);
-  float* topd = reinterpret_cast<float*>(w + b.off_topd);
-  int64_t* topr = reinterpret_cast<int64_t*>(w + b.off_topr);
   const int64_t nq_pad8 = (nq + 255) / 256 * 256;
+  // (the query prep also empties thr and zeroes the counts)
   int rc = launch_qprep8(Q, nq, nq_pad8, (int)d, b.dq, metric,
                          reinterpret_cast<int8_t*>(w + b.off_qh),
-                         reinterpret_cast<float*>(w + b.off_qinfo), st);
+                         reinterpret_cast<float*>(w + b.off_qinfo), st, thr, count);
   if (rc) return rc;
   if (metric == FX_METRIC_COS) {  // the scan's max(|q|, 1e-12) for the exact distances
     rc = launch_qnorm(Q, nq, (int)d, qnorm, st, 0);
     if (rc) return rc;
   }
-  const size_t count_bytes = (size_t)nq * 4 * kCountStride;
-  hipError_t e = hipMemsetAsync(thr, 0xFF, (size_t)nq * 8, st);
-  if (e == hipSuccess) e = hipMemsetAsync(count, 0, count_bytes, st);
-  if (e != hipSuccess) {
-    set_error("batched memset: %s", hipGetErrorString(e));
-    return FX_EHIP;
-  }
-  const bool merge_zeroes = b.merge.levels == 1;
   auto args = [&](int ph) {
     FilterArgs a = {};
     a.X = image;
@@ -627,13 +661,11 @@ static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, cons
     a.diag = diag_env("FX_FILTER_DIAG", 0);
     return a;
   };
-  // the exact k-th of the k best upper bounds in `keys` -> thr
+  // the exact k-th of the k best upper bounds in `keys` -> thr (one fused
+  // launch when the buffer fits one workgroup's LDS)
   auto exact_threshold = [&](const uint64_t* keys, bool zero) {
-    int r = run_merge(b.merge, keys, nq, k, w + b.off_merge, topd, topr, st, nullptr, nullptr, 0,
-                      count, zero);
-    if (r) return r;
-    return launch_exact_kth(X, dtype, n, (int)d, row_base, Q, qnorm, nq, (int)k, topr, metric,
-                            thr, st);
+    return launch_exact_threshold(X, dtype, n, (int)d, row_base, Q, qnorm, nq, keys, b.cap, count,
+                                  zero, (int)k, metric, thr, st);
   };
   const int m = b.nphases;
   for (int ph = 0; ph + 2 < m; ++ph) {  // sampling phases: thresholds only
@@ -642,14 +674,10 @@ static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, cons
     a.ub_test = ph > 0 && option(kOptBatchUbTest) != 0 ? 1 : 0;
     rc = launch_filter(a, metric, st);
     if (rc) return rc;
+    // (both reset the counts they read: the next phase appends from 0)
     rc = ph + 3 == m ? exact_threshold(cand, true)
-                     : run_merge(b.merge, cand, nq, k, w + b.off_merge, nullptr, nullptr, st, thr,
-                                 nullptr, 0, count, true);
+                     : launch_sample_threshold(cand, nq, b.cap, count, true, (int)k, thr, st);
     if (rc) return rc;
-    if (!merge_zeroes && (e = hipMemsetAsync(count, 0, count_bytes, st)) != hipSuccess) {
-      set_error("batched memset: %s", hipGetErrorString(e));
-      return FX_EHIP;
-    }
   }
   // F1: the last sample's tiles (with one phase: every tile), both bounds
   FilterArgs f1 = args(m >= 2 ? m - 2 : 0);
@@ -838,7 +866,7 @@ static int search_layout(const void* corpus, int dtype, int64_t n, int64_t d, in
 // a filter image applies to rows of whole 16-B pieces (d % 8 == 0) through
 // the filter: an fp16 image to f32 rows, an int8 image to f32 or f16 rows
 static bool image_applies(const SearchLayout& s, int dtype, int64_t d, bool img8, int64_t k) {
-  if (img8 && k > kI8MaxK) return false;
+  if (img8 && k > i8_max_k()) return false;
   return s.batched && s.batch.filter && d % 8 == 0 &&
          (dtype == FX_DTYPE_F32 || (img8 && dtype == FX_DTYPE_F16));
 }
@@ -871,10 +899,11 @@ static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_
       if (img && img8) {  // int8 image: denser samples (filter_phases)
         BatchLayout b = s.batch;
         const int64_t rmax = b.cap / (4 * k);
-        int64_t r = rmax < kI8SampleRatio ? rmax : kI8SampleRatio;
+        int64_t r1 = rmax < kI8SampleRatio ? rmax : kI8SampleRatio;
+        int64_t r2 = rmax < kI8GrowRatio ? rmax : kI8GrowRatio;
         const int64_t v = option(kOptBatchRatio);  // test switch: any ratio up to rmax
-        if (v >= 2) r = v < rmax ? v : rmax;
-        rc = plan_phases(&b, filter_tile_rows(dtype), r);
+        if (v >= 2) r1 = r2 = v < rmax ? v : rmax;
+        rc = plan_phases_i8(&b, filter_tile_rows(dtype), r1, r2);
         if (rc) return rc;
         return filter_phases_i8(b, corpus, dtype, image, rowinfo, n, d, row_base, queries, nq,
                                 metric, k, mask, reinterpret_cast<char*>(ws), st);
@@ -1086,8 +1115,11 @@ static int reduce_impl(const void* corpus, int dtype, int64_t n, int64_t d, int6
   char* w = reinterpret_cast<char*>(ws);
   const uint64_t* cand = reinterpret_cast<const uint64_t*>(w + b.off_cand);
   uint32_t* count = reinterpret_cast<uint32_t*>(w + b.off_count);
-  rc = run_merge(b.merge, cand, nq, k, w + b.off_merge, out_dist, out_row, st, nullptr, nullptr,
-                 0, count);  // (the fallback gate reads the counts next: kept)
+  // (the fallback gate reads the counts next: kept)
+  rc = b.img8 ? launch_final_select(cand, nq, b.cap, count, (int)k, out_dist, out_row, nullptr, 0,
+                                    st)
+              : run_merge(b.merge, cand, nq, k, w + b.off_merge, out_dist, out_row, st, nullptr,
+                          nullptr, 0, count);
   if (rc) return rc;
   // queries whose candidates overflowed `cap`: recomputed exactly, gated on
   // the device ("force_fallback" (test switch): every query)

@@ -24,6 +24,7 @@ enum Option : int {
   kOptFilterImage,  // filter image bits for f32 corpora (engine policy): 8, 16 or 0 (none)
   kOptBatchUbTest,  // sampling phases append by upper bound (0: by lower bound, test switch)
   kOptSingleImage,  // single queries over large f32 corpora through a supplied int8 image
+  kOptI8MaxK,       // largest k an int8 filter image serves
   kOptCount
 };
 int64_t option(Option o);
@@ -139,6 +140,24 @@ int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_bas
                      const float* Q, const float* qnorm, int64_t nq, int k, int64_t* rows,
                      int metric, uint64_t* thr, hipStream_t stream);
 
+// run_merge (top-k by key of each query's first count[q] entries of keys
+// [nq][cap]) + launch_exact_kth in one launch, any cap (knn_batch.hip
+// select_kernel, streaming over LDS-sized chunks)
+int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t row_base,
+                           const float* Q, const float* qnorm, int64_t nq, const uint64_t* keys,
+                           int64_t cap, uint32_t* count, bool zero_count, int k, int metric,
+                           uint64_t* thr, hipStream_t stream);
+// thr[q] = min(thr[q], the k-th smallest of the query's first count[q] keys)
+// when it has at least k (run_merge's threshold-only level, any cap)
+int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint32_t* count,
+                            bool zero_count, int k, uint64_t* thr, hipStream_t stream);
+// the final top-k of each query's first count[q] exact composites of keys
+// [nq][cap], sorted and decoded (run_merge's last level, one workgroup per
+// query, any cap); gate / gate_cap as ScanArgs::gate
+int launch_final_select(const uint64_t* keys, int64_t nq, int64_t cap, const uint32_t* count,
+                        int k, float* out_dist, int64_t* out_row, const uint32_t* gate,
+                        int64_t gate_cap, hipStream_t stream);
+
 // Batched filter on the fp16 matrix cores (knn_filter.hip): appends every
 // (row, query) whose rigorous lower bound reaches the query's threshold.
 struct FilterArgs {
@@ -211,8 +230,11 @@ __device__ __forceinline__ uint32_t perm_row(uint64_t a, int64_t n, int64_t i) {
 // and the exact scan recomputes it, fx_knn_reduce's gated fallback)
 int launch_overflow_gate(const uint64_t* cand, uint32_t* count, const uint64_t* thr, int64_t nq,
                          int cap, int64_t num, int64_t den, hipStream_t stream);
+// (thr, count: when given, each query's threshold is set empty and its append
+// count zeroed in the same launch)
 int launch_qprep8(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
-                  int8_t* Qb, float* qinfo, hipStream_t stream);
+                  int8_t* Qb, float* qinfo, hipStream_t stream, uint64_t* thr = nullptr,
+                  uint32_t* count = nullptr);
 int launch_qprep(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
                  uint16_t* Qh, float* qinfo, hipStream_t stream);
 int filter_tile_rows(int dtype);

@@ -25,6 +25,7 @@
 // with it never drops a true top-k row (capi.hip: batched_search).  The
 // buffers are then reduced by the ordinary merge kernels.
 #include "fx_internal.h"
+#include "fx_select.h"
 #include "fx_wave.h"
 
 namespace fx {
@@ -528,6 +529,223 @@ int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_bas
   hipLaunchKernelGGL(kth_max_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, stream,
                      reinterpret_cast<const uint64_t*>(rows), nq, k, thr);
   return check_launch("kth_max_kernel");
+}
+
+// One workgroup per query selects the k smallest keys among the query's
+// first count[q] entries of keys [nq][cap] (a streaming block_keep_k over
+// LDS-sized chunks, the k kept so far carried into the next chunk: any
+// count in one launch), then
+//   MODE 0 (exact threshold): their exact distances (exact_distance16, 64
+//     groups of 16 lanes) and thr[q] = min(thr[q], the largest exact
+//     composite) -- run_merge + launch_exact_kth in one launch; a query with
+//     fewer than k candidates keeps its threshold;
+//   MODE 1 (final select): the k smallest (exact composites after
+//     launch_rescore) bitonic-sorted and decoded to (distance, row), the
+//     last level of run_merge; gate / gate_cap as ScanArgs::gate;
+//   MODE 2 (sample threshold): thr[q] = min(thr[q], the k-th smallest key)
+//     when there are at least k (run_merge's threshold-only level).
+// zero_count resets the count once every thread has read it.
+constexpr int kSelectThreads = 1024;
+constexpr int kSelectEntries = 16384;  // LDS chunk (128 KB)
+template <typename T, int METRIC, int MODE>
+__global__ void __launch_bounds__(kSelectThreads)
+    select_kernel(const T* __restrict__ X, int64_t n, int d, int64_t row_base,
+                  const float* __restrict__ Q, const float* __restrict__ qnorm,
+                  const uint64_t* __restrict__ keys, int64_t cap, uint32_t* __restrict__ count,
+                  int zero_count, int k, int P2, uint64_t* __restrict__ thr,
+                  float* __restrict__ out_dist, int64_t* __restrict__ out_row,
+                  const uint32_t* __restrict__ gate, int64_t gate_cap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  MergeShared* ms = reinterpret_cast<MergeShared*>(smem);
+  uint64_t* res = reinterpret_cast<uint64_t*>(smem + sizeof(MergeShared));
+  uint64_t* s = res + P2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int64_t q = blockIdx.y;
+  if (gate != nullptr && (int64_t)gate[q * kCountStride] <= gate_cap) return;
+  const uint32_t c = count[q * kCountStride];
+  const int64_t m = (int64_t)c < cap ? (int64_t)c : cap;
+  __syncthreads();
+  if (zero_count && tid == 0) count[q * kCountStride] = 0u;
+  if (MODE != 1 && m < k) return;  // (uniform) fewer than k candidates: no threshold
+  const uint64_t* src = keys + q * cap;
+  int nres = 0;
+  const int64_t chunk = kSelectEntries - k;
+  for (int64_t off = 0; off < m || (off == 0 && m == 0); off += chunk) {  // (uniform)
+    const int cnt = (int)((m - off) < chunk ? (m - off) : chunk);
+    block_reset(ms);
+    __syncthreads();
+    uint64_t v_or = 0, v_and = ~0ull;
+    for (int base = tid; base < cnt; base += kSelectThreads * 8) {
+      uint64_t e[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = base + j * kSelectThreads;
+        e[j] = i < cnt ? src[off + i] : kEmpty;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = base + j * kSelectThreads;
+        if (i < cnt) {
+          s[i] = e[j];
+          v_or |= e[j];
+          v_and &= e[j];
+        }
+      }
+    }
+    for (int i = tid; i < nres; i += kSelectThreads) {  // the k kept so far
+      const uint64_t e = res[i];
+      s[cnt + i] = e;
+      v_or |= e;
+      v_and &= e;
+    }
+    const int t = cnt + nres;
+    block_or_and(v_or, v_and, ms);
+    __syncthreads();
+    if (t > k) {
+      block_keep_k<kSelectThreads>(s, t, k, res, ms);
+      nres = k;
+    } else {
+      for (int i = tid; i < t; i += kSelectThreads) res[i] = s[i];
+      nres = t;
+    }
+    __syncthreads();
+    if (m == 0) break;
+  }
+  if constexpr (MODE == 2) {
+    uint64_t mx = 0ull;  // (nres == k: m >= k)
+    for (int i = tid; i < nres; i += kSelectThreads) mx = res[i] > mx ? res[i] : mx;
+    mx = wave_max_u64(mx);
+    if (tid == 0) ms->shmax = 0ull;
+    __syncthreads();
+    if (lane == 0) atomicMax(&ms->shmax, (unsigned long long)mx);
+    __syncthreads();
+    if (tid == 0 && ms->shmax < thr[q]) thr[q] = ms->shmax;
+  } else if constexpr (MODE == 0) {
+    if (tid == 0) ms->shmax = 0ull;
+    __syncthreads();
+    const int grp = tid >> 4, jl = tid & 15;
+    const float* qv = Q + q * (int64_t)d;
+    const float qn = METRIC == 2 ? qnorm[q] : 0.f;
+    uint64_t mx = 0ull;
+    for (int j0 = 0; j0 < k; j0 += kSelectThreads / 16) {  // (uniform trip count)
+      const int j = j0 + grp;
+      const uint64_t e = j < nres ? res[j] : kEmpty;
+      const int64_t grow = (int64_t)(e & 0xffffffffull);
+      const int64_t row = grow - row_base;
+      const bool live = j < nres && e != kEmpty && row >= 0 && row < n;
+      const float dist = exact_distance16<T, METRIC>(X + (live ? row : 0) * (int64_t)d, qv, d,
+                                                     jl, live, qn);
+      // a missing or out-of-shard row: the largest composite (no threshold)
+      const uint64_t comp = live ? make_comp(dist, (uint32_t)grow) : kEmpty;
+      if (j < k) mx = comp > mx ? comp : mx;
+    }
+    mx = wave_max_u64(mx);
+    if (lane == 0) atomicMax(&ms->shmax, (unsigned long long)mx);
+    __syncthreads();
+    if (tid == 0 && ms->shmax < thr[q]) thr[q] = ms->shmax;
+  } else {
+    for (int i = nres + tid; i < P2; i += kSelectThreads) res[i] = kEmpty;
+    __syncthreads();
+    for (int size = 2; size <= P2; size <<= 1) {  // bitonic sort of res[0..P2)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = tid; i < (P2 >> 1); i += kSelectThreads) {
+          const int lo = (i / stride) * 2 * stride + (i % stride);
+          const int hi = lo + stride;
+          const bool asc = (lo & size) == 0;
+          const uint64_t x = res[lo], y = res[hi];
+          if ((x > y) == asc) {
+            res[lo] = y;
+            res[hi] = x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (int i = tid; i < k; i += kSelectThreads) {
+      const uint64_t e = res[i];
+      out_dist[q * k + i] = e == kEmpty ? __builtin_nanf("") : key_float((uint32_t)(e >> 32));
+      out_row[q * k + i] = e == kEmpty ? -1 : (int64_t)(e & 0xffffffffull);
+    }
+  }
+}
+
+template <typename T, int MODE>
+static int launch_select_t(const T* X, int64_t n, int d, int64_t row_base, const float* Q,
+                           const float* qnorm, int64_t nq, const uint64_t* keys, int64_t cap,
+                           uint32_t* count, int zero, int k, int metric, uint64_t* thr,
+                           float* out_dist, int64_t* out_row, const uint32_t* gate,
+                           int64_t gate_cap, hipStream_t stream) {
+  const void* fn = metric == FX_METRIC_COS  ? (const void*)select_kernel<T, 2, MODE>
+                   : metric == FX_METRIC_IP ? (const void*)select_kernel<T, 1, MODE>
+                                            : (const void*)select_kernel<T, 0, MODE>;
+  if (int rc = allow_lds(fn)) return rc;
+  int P2 = 1;
+  while (P2 < k) P2 <<= 1;
+  const size_t smem = sizeof(MergeShared) + ((size_t)P2 + kSelectEntries) * 8;
+  for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
+    const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
+    const T* x = X;
+    const float* qv = Q != nullptr ? Q + q0 * d : nullptr;
+    const float* qnm = qnorm != nullptr ? qnorm + q0 : nullptr;
+    const uint64_t* kq = keys + q0 * cap;
+    uint32_t* cq = count + q0 * kCountStride;
+    uint64_t* tq = thr != nullptr ? thr + q0 : nullptr;
+    float* od = out_dist != nullptr ? out_dist + q0 * k : nullptr;
+    int64_t* orow = out_row != nullptr ? out_row + q0 * k : nullptr;
+    const uint32_t* gq = gate != nullptr ? gate + q0 * kCountStride : nullptr;
+    void* args[] = {(void*)&x,   (void*)&n,   (void*)&d,    (void*)&row_base, (void*)&qv,
+                    (void*)&qnm, (void*)&kq,  (void*)&cap,  (void*)&cq,       (void*)&zero,
+                    (void*)&k,   (void*)&P2,  (void*)&tq,   (void*)&od,       (void*)&orow,
+                    (void*)&gq,  (void*)&gate_cap};
+    hipError_t e = hipLaunchKernel(fn, dim3(1, (unsigned)qn), dim3(kSelectThreads), args, smem,
+                                   stream);
+    if (e != hipSuccess) {
+      set_error("select_kernel launch: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+  }
+  return check_launch("select_kernel");
+}
+
+int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t row_base,
+                           const float* Q, const float* qnorm, int64_t nq, const uint64_t* keys,
+                           int64_t cap, uint32_t* count, bool zero_count, int k, int metric,
+                           uint64_t* thr, hipStream_t stream) {
+  if (k > kSelectEntries / 2 || k > cap) {
+    set_error("exact threshold: k %d beyond cap %lld", k, (long long)cap);
+    return FX_EUNSUPPORTED;
+  }
+  if (dtype == FX_DTYPE_F16)
+    return launch_select_t<_Float16, 0>(reinterpret_cast<const _Float16*>(X), n, d, row_base, Q,
+                                        qnorm, nq, keys, cap, count, zero_count ? 1 : 0, k, metric,
+                                        thr, nullptr, nullptr, nullptr, 0, stream);
+  return launch_select_t<float, 0>(reinterpret_cast<const float*>(X), n, d, row_base, Q, qnorm, nq,
+                                   keys, cap, count, zero_count ? 1 : 0, k, metric, thr, nullptr,
+                                   nullptr, nullptr, 0, stream);
+}
+
+int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint32_t* count,
+                            bool zero_count, int k, uint64_t* thr, hipStream_t stream) {
+  if (k > kSelectEntries / 2) {
+    set_error("sample threshold: k %d too large", k);
+    return FX_EUNSUPPORTED;
+  }
+  return launch_select_t<float, 2>(nullptr, 0, 1, 0, nullptr, nullptr, nq, keys, cap, count,
+                                   zero_count ? 1 : 0, k, FX_METRIC_L2, thr, nullptr, nullptr,
+                                   nullptr, 0, stream);
+}
+
+int launch_final_select(const uint64_t* keys, int64_t nq, int64_t cap, const uint32_t* count,
+                        int k, float* out_dist, int64_t* out_row, const uint32_t* gate,
+                        int64_t gate_cap, hipStream_t stream) {
+  if (k > kSelectEntries / 2) {
+    set_error("final select: k %d too large", k);
+    return FX_EUNSUPPORTED;
+  }
+  // (MODE 1 reads no rows: the keys are exact composites already)
+  return launch_select_t<float, 1>(nullptr, 0, 1, 0, nullptr, nullptr, nq, keys, cap,
+                                   const_cast<uint32_t*>(count), 0, k, FX_METRIC_L2, nullptr,
+                                   out_dist, out_row, gate, gate_cap, stream);
 }
 
 }  // namespace fx

@@ -3681,10 +3681,15 @@ int launch_image8(const void* X, int dtype, int64_t n, int d, void* img, float* 
 // integer image exceeds norm 2048: R' = +inf (forced).
 __global__ void qprep8_kernel(const float* __restrict__ Q, int64_t nq, int64_t nq_pad, int d,
                               int dq, int metric, int8_t* __restrict__ Qb,
-                              float* __restrict__ qinfo) {
+                              float* __restrict__ qinfo, uint64_t* __restrict__ thr,
+                              uint32_t* __restrict__ count) {
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (q >= nq_pad) return;
+  if (q < nq && lane == 0) {  // (the search's threshold and append count, when given)
+    if (thr != nullptr) thr[q] = ~0ull;
+    if (count != nullptr) count[q * kCountStride] = 0u;
+  }
   auto at = [&](int i) -> int8_t& {
     return Qb[((int64_t)(i >> 6) * nq_pad + q) * 64 + (i & 63)];
   };
@@ -3750,9 +3755,9 @@ __global__ void qprep8_kernel(const float* __restrict__ Q, int64_t nq, int64_t n
 }
 
 int launch_qprep8(const float* Q, int64_t nq, int64_t nq_pad, int d, int dq, int metric,
-                  int8_t* Qb, float* qinfo, hipStream_t stream) {
+                  int8_t* Qb, float* qinfo, hipStream_t stream, uint64_t* thr, uint32_t* count) {
   hipLaunchKernelGGL(qprep8_kernel, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, stream, Q,
-                     nq, nq_pad, d, dq, metric, Qb, qinfo);
+                     nq, nq_pad, d, dq, metric, Qb, qinfo, thr, count);
   return check_launch("qprep8_kernel");
 }
 

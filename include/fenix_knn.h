@@ -87,6 +87,8 @@ int fx_device_count(int* out);
  *                            bound reaches the threshold (0: lower bound)
  *   "single_query_image"  1  0: single queries keep the exact scan even when
  *                            an int8 filter image is supplied
+ *   "i8_max_k"          256  largest k an int8 filter image serves (larger k:
+ *                            the fp16 image / f32 rows, or the exact scan)
  *   "force_fallback"      0  1: every batched query is recomputed by the exact
  *                            single-query scan, as if its candidates overflowed
  *   "scan_interleave"    -1  -1: by row size; 0: one row range per workgroup;
