@@ -304,31 +304,33 @@ static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, 
 // Nested row samples of the batched phases: phase i scans every stride_i-th
 // tile of tr rows, each stride a multiple r of the next, the first at most
 // cap rows, the last every tile.
-// The int8 image's plan (filter_phases_i8): the last sample takes every
-// r1-th tile (F1, its complement is F2), the ones before it grow by r2
-// (their appends stay far below cap: about r2 k upper bounds per query),
-// the first holds at most cap rows.  10M x 768, r1 = 8, r2 = 16: 20, 306,
-// 4 883 tiles + the 34 180 F2 reads.
+// The int8 image's plan (filter_phases_i8).  The image stores its rows in a
+// permuted order (image8_perm: a Weyl sequence over the corpus), so any
+// PREFIX of its tiles is an equidistributed sample of the corpus: the
+// samples are nested prefixes, read as contiguous runs.  The last sample F1
+// holds ceil(tiles / r1) tiles (F2 reads the rest), the ones before it
+// shrink by r2 (their appends stay far below cap: about r2 k upper bounds
+// per query), the first holds at most cap rows.  10M x 768, r1 = 8, r2 = 16:
+// 20, 306, 4 883 tiles, then F2's 34 180.
 static int plan_phases_i8(BatchLayout* b, int64_t tr, int64_t r1, int64_t r2) {
-  int64_t strides[16];
+  int64_t nums[16];
   int m = 0;
-  strides[m++] = 1;
+  nums[m++] = b->tiles;
   int64_t r = r1;
-  while ((b->tiles + strides[m - 1] - 1) / strides[m - 1] * tr > b->cap) {
+  while (nums[m - 1] * tr > b->cap) {
     if (m >= 15) {
       set_error("batched sampling plan too deep");
       return FX_EUNSUPPORTED;
     }
-    strides[m] = strides[m - 1] * r;
+    nums[m] = (nums[m - 1] + r - 1) / r;
     ++m;
     r = r2;
   }
   b->nphases = m;
   for (int i = 0; i < m; ++i) {
-    const int64_t st = strides[m - 1 - i];
-    b->stride[i] = st;
+    b->num[i] = nums[m - 1 - i];
     b->start[i] = 0;
-    b->num[i] = (b->tiles + st - 1) / st;
+    b->stride[i] = 1;
   }
   return FX_OK;
 }
@@ -603,16 +605,17 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
 //     later ones the upper bounds at or below the previous threshold; the k-th
 //     upper bound is the next threshold, and after phase m-3 the exact
 //     distances of the k best upper bounds (launch_exact_kth) set it;
-//   F1 (phase m-2, the last sample's tiles): every pair whose lower bound
+//   F1 (phase m-2, the last sample's prefix of tiles): every pair whose lower bound
 //     reaches that threshold, appended with both bounds into the final
 //     candidate buffer; the exact k-th of its k best upper bounds is the
 //     next, much tighter threshold;
 //   overflow gate: F1's candidates under the new threshold, scaled to the
 //     tiles left, predict the final count; a query predicted past cap skips
 //     the final pass and goes to the exact scan (fx_knn_reduce's fallback);
-//   F2 (phase m-1): every tile F1 did not read, lower bound against the new
-//     threshold, appended after F1's candidates.  Each image row is read
-//     once by F1 or F2 (the sampling phases re-read 1/r^2 + ... of them);
+//   F2 (phase m-1): the tiles after F1's prefix, lower bound against the
+//     new threshold, appended after F1's candidates.  Each image row is
+//     read once by F1 or F2 (the sampling phases re-read 1/r1 (1/r2 + ...)
+//     of them);
 //   the exact k-th of all candidates' k best upper bounds is the final
 //     threshold, and the candidates whose lower bound reaches it are
 //     rescored exactly (launch_rescore), fx_knn_reduce selects the top k.
@@ -692,10 +695,10 @@ static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, cons
     if (t2 > 0) {
       rc = launch_overflow_gate(cand, count, thr, nq, (int)b.cap, t2, t1, st);
       if (rc) return rc;
-      // F2: the tiles F1 did not read (plan tile p -> p + p / (r - 1) + 1)
+      // F2: the tiles after F1's prefix
       FilterArgs f2 = args(m - 1);
+      f2.tile_start = t1;
       f2.num_tiles = t2;
-      f2.tile_skip = b.stride[m - 2];
       f2.cand_ub = cand_ub;
       f2.skip_full = 1;
       rc = launch_filter(f2, metric, st);

@@ -186,8 +186,6 @@ struct FilterArgs {
                           // launch_qprep8
   int all_pass;           // no query has a threshold yet (thr all empty): img8 appends
                           // every live pair without the test
-  int64_t tile_skip;      // > 1: the plan's tiles skip every tile_skip-th tile (img8 final
-                          // pass: the last sample's tiles were read with its threshold)
   int skip_full;          // a workgroup whose queries all hold count > cap returns at once
   uint64_t perm_a;        // img8: image row i holds corpus row (perm_a * i) % n (image8_perm)
   int ub_test;            // sampling phase after the first: append when the UPPER bound

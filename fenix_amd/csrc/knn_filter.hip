@@ -1639,13 +1639,8 @@ __global__ void __launch_bounds__(kI3Threads, 2) filter_img3_kernel(FilterArgs a
   const int64_t ntile32 = (a.n + 31) / 32;
   // workgroup tiles: kI3Sub per fBM-row tile of the plan (a.tile_start, ...)
   const int64_t ntiles = a.num_tiles * kI3Sub;
-  // (tile_skip > 1: plan tile p maps past every tile_skip-th tile, the ones
-  // the last sample read)
-  const int64_t skip1 = a.tile_skip > 1 ? a.tile_skip - 1 : 0;
   auto tile_r0 = [&](int64_t ti) {
-    int64_t pt = a.tile_start + (ti / kI3Sub) * a.tile_stride;
-    if (skip1 > 0) pt += pt / skip1 + 1;
-    return pt * fBM + (ti % kI3Sub) * kI3BM;
+    return (a.tile_start + (ti / kI3Sub) * a.tile_stride) * fBM + (ti % kI3Sub) * kI3BM;
   };
   if ((int64_t)blockIdx.x >= ntiles) return;
   if (a.skip_full) {  // every query of the tile predicted to overflow: nothing to do
@@ -1991,6 +1986,7 @@ static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
   }
   return check_launch("filter_img3_kernel");
 }
+
 #endif  // FX_FILTER_IMG3
 
 #if FX_FILTER_IMG3
