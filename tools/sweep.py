@@ -3,7 +3,9 @@
     python tools/sweep.py [--libs new,old] [--reps 2] [--steps 10] [--warmup 2]
                           [--out gpurun_out/sweep.jsonl] -- "ARGS1" "ARGS2" ...
 
-Each quoted ARGS is one bench.py configuration; every (rep, config, lib) runs
+Each quoted ARGS is one bench.py configuration (leading NAME=VALUE tokens are
+environment variables for that run, e.g. "FX_FILTER_DIAG=2 --nq 256" with
+``--libs diag`` for the diagnostic build's switches); every (rep, config, lib) runs
 bench.py in its own process under a time limit (``--no-cpu-baseline`` added),
 and one line per run is printed and appended to ``--out``.  A library NAME
 other than ``new`` is ``fenix_amd/lib/libfenix_knn_NAME.so`` (loaded through
@@ -54,8 +56,12 @@ def main() -> int:
                 if lib != "new":
                     env["FENIX_AMD_LIB"] = os.path.join(ROOT, "fenix_amd", "lib",
                                                         f"libfenix_knn_{lib}.so")
+                toks = shlex.split(cfg)
+                while toks and "=" in toks[0] and toks[0].split("=", 1)[0].isupper():
+                    key, val = toks.pop(0).split("=", 1)
+                    env[key] = val
                 cmd = ["timeout", "-k", "10", str(a.timeout), sys.executable, "-u",
-                       os.path.join(ROOT, "bench.py"), *shlex.split(cfg), "--steps",
+                       os.path.join(ROOT, "bench.py"), *toks, "--steps",
                        str(a.steps), "--warmup", str(a.warmup), "--no-cpu-baseline"]
                 r = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, env=env)
                 if r.returncode != 0:
