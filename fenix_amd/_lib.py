@@ -93,7 +93,7 @@ SYMBOLS = (
 # test switches
 OPTIONS = ("batched", "batch_min_queries", "batch_cap", "batch_sample_ratio", "force_fallback",
            "scan_interleave", "q8_dma", "filter_image", "batch_ub_test", "single_query_image",
-           "i8_max_k")
+           "i8_max_k", "img6")
 
 _lock = threading.Lock()
 _lib = None
@@ -254,18 +254,42 @@ def max_k() -> int:
     return int(load().fx_max_k())
 
 
+# Per-shape planning answers (workspace sizes, whether a search reads a filter
+# image) depend on the shape and the process options only: memoised, keyed on
+# the options' generation (set_option bumps it), so a serving loop over many
+# shards does not re-plan each search in Python-to-C calls.
+_opt_gen = 0
+_plan_cache: dict = {}
+_PLAN_CACHE_MAX = 4096
+
+
+def _planned(key: tuple, compute):
+    hit = _plan_cache.get((_opt_gen, key))
+    if hit is None:
+        if len(_plan_cache) >= _PLAN_CACHE_MAX:
+            _plan_cache.clear()
+        hit = _plan_cache[(_opt_gen, key)] = compute()
+    return hit
+
+
 def knn_workspace_bytes(n: int, d: int, dtype: int, nq: int, k: int) -> int:
-    out = ctypes.c_size_t(0)
-    check(load().fx_knn_workspace_bytes(n, d, dtype, nq, k, ctypes.byref(out)))
-    return int(out.value)
+    def compute() -> int:
+        out = ctypes.c_size_t(0)
+        check(load().fx_knn_workspace_bytes(n, d, dtype, nq, k, ctypes.byref(out)))
+        return int(out.value)
+
+    return _planned(("ws", n, d, dtype, nq, k), compute)
 
 
 def filter_image_used(n: int, d: int, dtype: int, nq: int, k: int, metric: int) -> bool:
     """True when a search of this shape runs the batched filter over f32 rows,
     which then streams an fp16 filter image if one is given (fx_filter_image)."""
-    out = ctypes.c_int(0)
-    check(load().fx_filter_image_used(n, d, dtype, nq, k, metric, ctypes.byref(out)))
-    return bool(out.value)
+    def compute() -> bool:
+        out = ctypes.c_int(0)
+        check(load().fx_filter_image_used(n, d, dtype, nq, k, metric, ctypes.byref(out)))
+        return bool(out.value)
+
+    return _planned(("img", n, d, dtype, nq, k, metric), compute)
 
 
 def image8_perm(n: int) -> int:
@@ -321,8 +345,11 @@ def search_ex_workspace_bytes(corpus: "Corpus", nrows: int, nq: int, k: int) -> 
 
 
 def set_option(name: str, value: int) -> None:
-    """fx_set_option: a process-wide library option (OPTIONS)."""
+    """fx_set_option: a process-wide library option (OPTIONS).  Options set
+    through the C ABI directly bypass the planning memo: use this."""
+    global _opt_gen
     check(load().fx_set_option(name.encode(), int(value)))
+    _opt_gen += 1
 
 
 def get_option(name: str) -> int:

@@ -25,6 +25,7 @@ enum Option : int {
   kOptBatchUbTest,  // sampling phases append by upper bound (0: by lower bound, test switch)
   kOptSingleImage,  // single queries over large f32 corpora through a supplied int8 image
   kOptI8MaxK,       // largest k an int8 filter image serves
+  kOptImg6,         // int8 images, > 64 queries: the resident-query-slice kernel (0: img3)
   kOptCount
 };
 int64_t option(Option o);

@@ -1987,6 +1987,208 @@ static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
   return check_launch("filter_img3_kernel");
 }
 
+#if FX_FILTER_BQ <= 128
+// ---- int8 image, a resident query slice (filter_img6_kernel)
+//
+// filter_img3_kernel streams the query tile through an LDS ring: every
+// 64-component chunk of every 256-row tile DMAs the tile's queries again
+// (as many bytes per chunk as the image itself) behind a workgroup barrier,
+// so the 8 waves run in lockstep and the MFMAs add to the image stream
+// instead of hiding under it.  Here a workgroup holds its
+// slice of 128 queries (the q128 build; 64 in q64i) in LDS for the whole kernel (96 KB at 768-d,
+// XOR-swizzled for conflict-free ds_read_b128) and each of its waves runs
+// alone: its own 32-row tiles, FX_I6_XS image k-steps in flight in registers
+// across tile ends, its own rows' terms and flags in LDS, the same epilogue
+// (i8_epilogue: pass test, bounds, LDS append segments shared through LDS
+// atomics).  No barrier between the prologue and the final segment flush.
+// A batch of more than 128 queries runs its slices on different CUs over
+// the same tiles at the same time -- workgroup (x, y) takes slice y and
+// tiles x, x + G, ... with G = CUs / slices, so the partners share an XCD
+// (x + G y = x mod 8) and the second read of a tile can come from its L2 or
+// the Infinity Cache instead of HBM.
+#ifndef FX_I6_XS
+#define FX_I6_XS 8
+#endif
+constexpr int kI6Waves = 8;
+constexpr int kI6Threads = 64 * kI6Waves;
+constexpr int kI6BM = 32 * kI6Waves;
+static_assert(kI6BM == fBM, "one plan tile per workgroup tile");
+constexpr int kI6SEG = FX_I3_SEG;
+struct Img6Shared {
+  float rinfo[kI6BM];
+  float rterm[kI6BM];
+  float rext[kI6BM];
+  uint32_t rrow[kI6BM];
+  uint32_t rflags[kRowFlagWords];
+  f32x4 qtab[fBQ];
+  f32x4 qinf[fBQ];
+  uint32_t seg[fBQ + 3 * fBQ * kI6SEG];
+  uint32_t segbase[fBQ];
+};
+// the query slice follows: (dq / 64) chunks x 128 queries x 64 B
+static size_t img6_smem(int dq) { return sizeof(Img6Shared) + (size_t)(dq / 64) * fBQ * 64; }
+bool img6_fits(int dq) { return img6_smem(dq) <= 160 * 1024; }
+
+template <int METRIC>
+__global__ void __launch_bounds__(kI6Threads, 1) filter_img6_kernel(FilterArgs a) {
+  constexpr int XS = FX_I6_XS, SEG = kI6SEG;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Img6Shared* sh = reinterpret_cast<Img6Shared*>(smem);
+  unsigned char* qslice = smem + sizeof(Img6Shared);
+#ifdef FX_DIAG_BUILD
+  const int diag = a.diag;
+#else
+  constexpr int diag = 0;
+#endif
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, l32 = lane & 31;
+  const int64_t q0 = (int64_t)blockIdx.y * fBQ;
+  const int ksteps = (a.d + 31) / 32;
+  const int nks = (ksteps + XS - 1) / XS * XS;  // (past the row end the image reads zeros)
+  const int ngroups = nks / XS;
+  const int64_t ntile32 = (a.n + 31) / 32;
+  const int64_t ntiles = a.num_tiles;
+  if ((int64_t)blockIdx.x >= ntiles) return;
+  i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, kI6Threads);
+  for (int q = tid; q < fBQ; q += kI6Threads) sh->seg[q] = 0u;
+  {  // the slice: chunk c of query Q at (c * 128 + Q) * 64, piece p at (p ^ ((Q >> 2) & 3)) * 16
+    const int nch = a.dq / 64;
+    const unsigned char* qb = reinterpret_cast<const unsigned char*>(a.Qh);
+    for (int i = tid; i < nch * fBQ * 4; i += kI6Threads) {
+      const int c = i / (fBQ * 4), Q = (i / 4) % fBQ, pc = i % 4;
+      const i32x4 v = *reinterpret_cast<const i32x4*>(
+          qb + ((int64_t)c * a.qstride + q0 + Q) * 64 + pc * 16);
+      *reinterpret_cast<i32x4*>(qslice + ((c * fBQ + Q) * 64 + ((pc ^ ((Q >> 2) & 3)) * 16))) = v;
+    }
+  }
+  __syncthreads();
+  // B fragment of query tile u at k-step ks: query Q = 32 u + l32, piece
+  // 2 (ks & 1) + h of chunk ks / 2 (bits 2-3 of Q do not depend on u)
+  const int bsw = (l32 >> 2) & 3;
+  auto bfrag = [&](int ks, int u) {
+    const int Q = 32 * u + l32;
+    return *reinterpret_cast<const f16x8*>(
+        qslice + ((ks >> 1) * fBQ + Q) * 64 + (((2 * (ks & 1) + h) ^ bsw) * 16));
+  };
+  auto tile_r0 = [&](int64_t ti) { return (a.tile_start + ti * a.tile_stride) * fBM; };
+  auto x_rsrc = [&](int64_t ti) {
+    const int64_t t32 = tile_r0(ti) / 32 + wid;
+    const int64_t live = (ti < ntiles && t32 < ntile32) ? 1 : 0;
+    const unsigned char* base = reinterpret_cast<const unsigned char*>(a.X) +
+                                (live ? t32 : 0) * (int64_t)ksteps * 1024;
+    const uint64_t xp = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xp >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)(live * ksteps * 1024));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             nb, 0x00020000);
+  };
+  const uint32_t xl = (uint32_t)opaque(lane) * 16u;
+  auto load_a = [&](__amdgpu_buffer_rsrc_t xr, int ks) {
+    const uint32_t off = ks < ksteps ? xl : 0x7fff0000u;
+    return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, off, ks * 1024, 2));
+  };
+  f32x16 acc[kI2QT];
+  const f32x16 acc0 = f32x16(kI8Magic);
+  auto mfma = [&](int u, const f16x8& xv, const f16x8& bv, bool start) {
+    typedef int i32x16 __attribute__((ext_vector_type(16)));
+    const f32x16 cin = start ? acc0 : acc[u];
+    acc[u] = __builtin_bit_cast(f32x16, __builtin_amdgcn_mfma_i32_32x32x32_i8(
+        __builtin_bit_cast(i32x4, xv), __builtin_bit_cast(i32x4, bv),
+        __builtin_bit_cast(i32x16, cin), 0, 0, 0));
+  };
+  // one k-step: its 4 B fragments first (one LDS wait), then the 4 MFMAs
+  auto kstep = [&](const f16x8& xv, int ks, bool start) {
+    f16x8 bv[kI2QT];
+#pragma unroll
+    for (int u = 0; u < kI2QT; ++u) bv[u] = bfrag(ks, u);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kI2QT; ++u) mfma(u, xv, bv[u], start);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const int lr = wid * 32 + l32;  // the wave's row this lane notes (lanes 0-31)
+  int64_t ti = blockIdx.x;
+  __amdgpu_buffer_rsrc_t xr = x_rsrc(ti);
+  f16x8 xa[XS];
+#pragma unroll
+  for (int s = 0; s < XS; ++s) xa[s] = load_a(xr, s);
+  for (; ti < ntiles; ti += gridDim.x) {
+    const int64_t r0 = tile_r0(ti);
+    const int64_t tn = ti + gridDim.x;
+    const __amdgpu_buffer_rsrc_t xn = x_rsrc(tn);
+    // this tile's row terms, early (lanes 0-31: row r0 + wid * 32 + l32)
+    const int64_t row = r0 + lr;
+    const int64_t rowc = row < a.n ? row : a.n - 1;
+    const f32x4 rsum = *reinterpret_cast<const f32x4*>(a.rowinfo + rowc * kI8RowInfo);
+    const uint32_t crow = perm_row(a.perm_a, a.n, rowc);
+    const uint32_t mword = a.mask != nullptr ? a.mask[crow >> 5] >> (crow & 31) : 1u;
+    // k-step groups of XS: the first starts the accumulators, the last
+    // refills from the next tile
+    for (int g = 0; g < ngroups; ++g) {
+      const bool last = g + 1 == ngroups;
+#pragma unroll
+      for (int s = 0; s < XS; ++s) {
+        const int ks = g * XS + s;
+        kstep(xa[s], ks, ks == 0);
+        xa[s] = last ? load_a(xn, s) : load_a(xr, ks + XS);
+      }
+    }
+    // the wave's 32 rows: terms, corpus rows and flags into its own LDS words
+    if (lane < 4) sh->rflags[(lane >> 1) * 16 + wid * 2 + (lane & 1)] = 0u;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (h == 0) {
+      const bool ok = row < a.n && (mword & 1u);
+      const float y1 = METRIC == 1 ? rsum[1] : METRIC == 2 ? rsum[2] : rsum[3];
+      i8_note_row(sh->rinfo, sh->rterm, sh->rext, sh->rflags, lr, rsum[0], y1, rsum[1], ok);
+      sh->rrow[lr] = (uint32_t)a.row_base + crow;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (!(diag & 2))
+      i8_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rext, sh->rrow, sh->rflags, sh->qtab,
+                          sh->qinf, a, q0, wid, h, l32, sh->seg, diag);
+    xr = xn;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  filter_flush_segments<SEG, kI6Threads>(sh->seg, sh->segbase, a, q0, tid);
+}
+
+int launch_img6(const FilterArgs& a, int metric, hipStream_t stream) {
+  if (a.num_tiles <= 0) return FX_OK;
+  const size_t smem = img6_smem(a.dq);
+  const void* fn = metric == FX_METRIC_COS  ? (const void*)filter_img6_kernel<2>
+                   : metric == FX_METRIC_IP ? (const void*)filter_img6_kernel<1>
+                                            : (const void*)filter_img6_kernel<0>;
+  if (int rc = allow_lds(fn)) return rc;
+  int cus = 0;
+  if (int rc = device_cus(&cus)) return rc;
+  const int64_t slices = (a.nq + fBQ - 1) / fBQ;
+  // every slice's workgroups co-resident (one per CU): slices x G <= CUs
+  int64_t bx = cus / (slices < cus ? slices : cus);
+  if (bx < 1) bx = 1;
+  if (bx > a.num_tiles) bx = a.num_tiles;
+  for (int64_t y0 = 0; y0 < slices; y0 += 65535) {
+    FilterArgs b = a;
+    const int64_t yn = (slices - y0) < 65535 ? (slices - y0) : 65535;
+    b.Qh = a.Qh + y0 * fBQ * 32;
+    b.qinfo = a.qinfo + y0 * fBQ * kI8QInfo;
+    b.thr = a.thr + y0 * fBQ;
+    b.count = a.count + y0 * fBQ * kCountStride;
+    b.cand = a.cand + y0 * fBQ * (int64_t)a.cap;
+    if (a.cand_ub) b.cand_ub = a.cand_ub + y0 * fBQ * (int64_t)a.cap;
+    b.nq = a.nq - y0 * fBQ;
+    void* args[] = {(void*)&b};
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(kI6Threads), args,
+                                   smem, stream);
+    if (e != hipSuccess) {
+      set_error("filter_img6_kernel launch: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+  }
+  return check_launch("filter_img6_kernel");
+}
+#endif  // FX_FILTER_BQ <= 128
 #endif  // FX_FILTER_IMG3
 
 #if FX_FILTER_IMG3
@@ -3243,9 +3445,13 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_
 }
 namespace q128 {
 int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_q128.hip
+int launch_img6(const FilterArgs& a, int metric, hipStream_t stream);
+bool img6_fits(int dq);
 }
-namespace q64i {
-int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_q64i.hip
+namespace q64i {  // knn_filter_q64i.hip
+int launch(const FilterArgs& a, int metric, hipStream_t stream);
+int launch_img6(const FilterArgs& a, int metric, hipStream_t stream);
+bool img6_fits(int dq);
 }
 namespace h256 {
 int launch(const FilterArgs& a, int metric, hipStream_t stream);  // knn_filter_h256.hip
@@ -3266,7 +3472,11 @@ bool filter_ring() { return diag_env("FX_FILTER_RING", 0) != 0; }
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
   // int8 images: filter_img3_kernel with 64-, 128- or 256-query tiles
   if (a.img8) {
-    if (a.nq <= 64) return q64i::launch(a, metric, stream);
+    if (a.nq <= 64) {
+      if (option(kOptImg6) >= 2 && q64i::img6_fits(a.dq)) return q64i::launch_img6(a, metric, stream);
+      return q64i::launch(a, metric, stream);
+    }
+    if (option(kOptImg6) != 0 && q128::img6_fits(a.dq)) return q128::launch_img6(a, metric, stream);
     if (a.nq <= 128) return q128::launch(a, metric, stream);
     return q256::launch(a, metric, stream);
   }
