@@ -70,6 +70,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true",
                    help="skip the result checks and the planted rows (diagnostic builds)")
+    p.add_argument("--no-batch-leg", action="store_true",
+                   help="skip the configs[2] batch leg (256 cosine queries over the same image)")
     p.add_argument("--no-accelerated", action="store_true",
                    help="skip the filter-image leg (profiling the exact scan alone)")
     p.add_argument("--cluster", type=int, default=0,
@@ -400,7 +402,7 @@ def main():
         if not args.no_verify:
             assert same, "the filter-image search differs from the exact scan"
         pass_bytes = img_bytes + nq * d * 4
-        a_traffic = pmc_traffic(f"{n}x{d}_{args.dtype}_{args.metric}_k{k}_q{nq}", "filter_img3",
+        a_traffic = pmc_traffic(f"{n}x{d}_{args.dtype}_{args.metric}_k{k}_q{nq}", "filter_img",
                                 _lib.library_sha())
         accel = {
             "what": "the product default for this search: int8 filter image + exact rescoring "
@@ -408,7 +410,7 @@ def main():
             "ms_per_step": a_el * 1e3 / args.steps,
             "vectors_per_s": n * world * nq * args.steps / a_el,
             "kernel_ms": a_ms,
-            "kernel": "fx::q64i::filter_img3_kernel (all phases) + thresholds + rescoring",
+            "kernel": "fx::q64i::filter_img6_kernel (all phases) + thresholds + rescoring",
             "image_bytes": img_bytes,
             "image_build_ms": image_build_ms,
             "bytes_per_search": pass_bytes,
@@ -419,6 +421,12 @@ def main():
             "bit_identical": same,
             "speedup_vs_headline": elapsed / a_el,
         }
+
+    # configs[2] beside it (BASELINE configs[2]: the same rows, a 256-query
+    # cosine batch through the same resident image), one rank only
+    batch = None
+    if single and image is not None and world == 1 and not args.no_batch_leg:
+        batch = batch_leg(eng, shard, image, img_bytes, n, d, k, args)
 
     total_rows = n * world
     value = total_rows * nq * args.steps / elapsed
@@ -431,13 +439,14 @@ def main():
         # rows (the rescoring reads a few thousand rows per query on top)
         scan_bytes = img_bytes + nq * d * 4
     if filt:
-        kname = (f"fx::filter_img3_kernel ({'int8' if bits == 8 else 'fp16'}-MFMA bound filter, "
+        kname = (f"fx::{'filter_img6_kernel' if bits == 8 and nq <= 128 else 'filter_img3_kernel'} "
+                 f"({'int8' if bits == 8 else 'fp16'}-MFMA bound filter, "
                  "all sample phases) + exact rescoring of the candidates")
     elif qu8:
         kname = "fx::scan_kernel<uint8> (quint8 codes dequantised in registers) + merge"
     else:
         kname = "fx::scan_kernel (fused distance + per-wave top-k)"
-    traffic = pmc_traffic(tag, "filter_img3" if filt else "scan_kernel", _lib.library_sha())
+    traffic = pmc_traffic(tag, "filter_img" if filt else "scan_kernel", _lib.library_sha())
     achieved = scan_bytes / (scan_ms * 1e-3) / 1e9
     roof = {
         "bound": "hbm",
@@ -505,6 +514,7 @@ def main():
                if image is not None else {}),
             "roofline": roof,
             **({"accelerated_exact": accel} if accel is not None else {}),
+            **({"configs2": batch} if batch is not None else {}),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
@@ -512,6 +522,68 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return out
+
+
+def batch_leg(eng, shard, image, img_bytes, n, d, k, args, nb=256, mname="cosine"):
+    """BASELINE configs[2] on the bench's resident shard and filter image: a
+    256-query cosine batch (query seed 2), W warmup + K timed searches, HIP
+    events around each search's launches; three of its queries checked bit
+    for bit against the exact per-query scan."""
+    from fenix_amd import _lib
+
+    dev = shard.data.device
+    mb = _lib.METRICS[mname]
+    qb = torch.empty((nb, d), dtype=torch.float32, device=dev)
+    eng.fill(qb, seed=2)
+    bd = torch.empty((nb, k), dtype=torch.float32, device=dev)
+    br = torch.empty((nb, k), dtype=torch.int64, device=dev)
+
+    def one(ev=None):
+        if ev is not None:
+            ev[0].record()
+        st = eng.scan(shard, qb, mb, k)
+        eng.reduce(shard, qb, mb, k, st, bd, br)
+        if ev is not None:
+            ev[1].record()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    for _ in range(args.warmup):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one(ev[i])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    span = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    same = None
+    if not args.no_verify:
+        idx = [0, 1, nb - 1]
+        sub = qb[idx].contiguous()
+        sd = torch.empty((len(idx), k), dtype=torch.float32, device=dev)
+        sr = torch.empty((len(idx), k), dtype=torch.int64, device=dev)
+        with _lib.options(batched=0, single_query_image=0):
+            st = eng.scan(shard, sub, mb, k)
+            eng.reduce(shard, sub, mb, k, st, sd, sr)
+        same = bool(np.array_equal(sr.cpu().numpy(), br[idx].cpu().numpy()) and np.array_equal(
+            sd.cpu().numpy().view(np.uint32), bd[idx].cpu().numpy().view(np.uint32)))
+        assert same, "configs[2] batch differs from the exact scan"
+    pass_bytes = img_bytes + nb * d * 4
+    return {
+        "workload": f"{n}x{d} f32 {mname} kNN k={k}, {nb}-query batch (query seed 2), "
+                    "same shard and filter image",
+        "ms_per_step": el * 1e3 / args.steps,
+        "vectors_per_s": n * nb * args.steps / el,
+        "kernel_ms": span,
+        "kernel": "filter phases (int8 MFMA bound filter) + thresholds + rescoring + select",
+        "bytes_per_search": pass_bytes,
+        "achieved_gbs_over_image": pass_bytes / (span * 1e-3) / 1e9,
+        "frac_over_image": pass_bytes / (span * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "mfma_tflops": 2.0 * n * nb * d / (span * 1e-3) / 1e12,
+        "mfma_peak_tflops": MFMA_F16_PEAK_TFS * 2,
+        "sample_bit_identical": same,
+    }
 
 
 class _nullctx:

@@ -454,6 +454,31 @@ static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, i
 }
 
 
+// The fallback's gated scan alone over all nq queries (s.fb_queries >= nq):
+// per overflowing query nlists lists of k composites at *lists, [nq][nlists k]
+static int fallback_scan(const SearchLayout& s, const void* corpus, int64_t n, int64_t d,
+                         int64_t row_base, const float* queries, int64_t nq, int64_t k,
+                         const uint32_t* mask, const uint32_t* count, int64_t gate_cap, char* ws,
+                         hipStream_t st, const uint64_t** lists) {
+  ScanArgs a = {};
+  a.X = corpus;
+  a.n = n;
+  a.d = (int)d;
+  a.row_base = row_base;
+  a.mask = mask;
+  a.rows_per_block = s.scan.rows_per_block;
+  a.k = (int)k;
+  a.cap = s.scan.cap;
+  a.qbytes = s.scan.qbytes;
+  a.mode = kModeTopk;
+  a.out_lists = reinterpret_cast<uint64_t*>(ws);
+  a.gate_cap = gate_cap;
+  a.q = queries;
+  a.gate = count;
+  *lists = a.out_lists;
+  return launch_scan(s.scan, a, nq, st);
+}
+
 // Batched-path fallback: the exact single-query scan + merge of every query
 // whose final candidates overflowed the buffer (count[q] > gate_cap; all of
 // them when gate_cap < 0), in rounds of s.fb_queries.  Decided on the device:
@@ -1118,18 +1143,27 @@ static int reduce_impl(const void* corpus, int dtype, int64_t n, int64_t d, int6
   char* w = reinterpret_cast<char*>(ws);
   const uint64_t* cand = reinterpret_cast<const uint64_t*>(w + b.off_cand);
   uint32_t* count = reinterpret_cast<uint32_t*>(w + b.off_count);
+  // queries whose candidates overflowed `cap` are recomputed exactly, gated
+  // on the device ("force_fallback" (test switch): every query)
+  const int64_t gate_cap = option(kOptForceFallback) != 0 ? -1 : b.cap;
+  if (b.img8 && s.fb_queries >= nq) {
+    // one round: the gated scan's lists feed the final select of the
+    // overflowing queries (no merge levels of their own)
+    const uint64_t* lists = nullptr;
+    rc = fallback_scan(s, corpus, n, d, row_base, queries, nq, k, mask, count, gate_cap,
+                       w + s.single_off, st, &lists);
+    if (rc) return rc;
+    return launch_final_select(cand, nq, b.cap, count, (int)k, out_dist, out_row, lists,
+                               s.scan.nlists * k, gate_cap, st);
+  }
   // (the fallback gate reads the counts next: kept)
   rc = b.img8 ? launch_final_select(cand, nq, b.cap, count, (int)k, out_dist, out_row, nullptr, 0,
-                                    st)
+                                    0, st)
               : run_merge(b.merge, cand, nq, k, w + b.off_merge, out_dist, out_row, st, nullptr,
                           nullptr, 0, count);
   if (rc) return rc;
-  // queries whose candidates overflowed `cap`: recomputed exactly, gated on
-  // the device ("force_fallback" (test switch): every query)
-  const int64_t gate_cap = option(kOptForceFallback) != 0 ? -1 : b.cap;
-  return fallback_search(s, corpus, dtype, n, d, row_base, queries, nq, metric, k, mask,
-                         reinterpret_cast<const uint32_t*>(w + b.off_count), gate_cap,
-                         w + s.single_off, out_dist, out_row, st);
+  return fallback_search(s, corpus, dtype, n, d, row_base, queries, nq, metric, k, mask, count,
+                         gate_cap, w + s.single_off, out_dist, out_row, st);
 }
 
 int fx_knn_filter_state(const void* corpus, int dtype, int64_t n, int64_t d, int64_t nq,

@@ -25,7 +25,7 @@ enum Option : int {
   kOptBatchUbTest,  // sampling phases append by upper bound (0: by lower bound, test switch)
   kOptSingleImage,  // single queries over large f32 corpora through a supplied int8 image
   kOptI8MaxK,       // largest k an int8 filter image serves
-  kOptImg6,         // int8 images, > 64 queries: the resident-query-slice kernel (0: img3)
+  kOptImg6,         // int8 images: resident-query-slice kernel (1: <= 128 queries, 2: all, 0: off)
   kOptCount
 };
 int64_t option(Option o);
@@ -154,10 +154,11 @@ int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint3
                             bool zero_count, int k, uint64_t* thr, hipStream_t stream);
 // the final top-k of each query's first count[q] exact composites of keys
 // [nq][cap], sorted and decoded (run_merge's last level, one workgroup per
-// query, any cap); gate / gate_cap as ScanArgs::gate
+// query, any cap); a query whose count exceeds alt_gate selects from its
+// alt_m entries of alt ([nq][alt_m], the overflow fallback scan's lists)
 int launch_final_select(const uint64_t* keys, int64_t nq, int64_t cap, const uint32_t* count,
-                        int k, float* out_dist, int64_t* out_row, const uint32_t* gate,
-                        int64_t gate_cap, hipStream_t stream);
+                        int k, float* out_dist, int64_t* out_row, const uint64_t* alt,
+                        int64_t alt_m, int64_t alt_gate, hipStream_t stream);
 
 // Batched filter on the fp16 matrix cores (knn_filter.hip): appends every
 // (row, query) whose rigorous lower bound reaches the query's threshold.

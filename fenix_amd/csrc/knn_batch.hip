@@ -541,7 +541,9 @@ int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_bas
 //     fewer than k candidates keeps its threshold;
 //   MODE 1 (final select): the k smallest (exact composites after
 //     launch_rescore) bitonic-sorted and decoded to (distance, row), the
-//     last level of run_merge; gate / gate_cap as ScanArgs::gate;
+//     last level of run_merge; a query whose count exceeds alt_gate (it
+//     overflowed the buffer) selects from its alt_m entries of alt instead
+//     (the overflow fallback scan's lists, [nq][alt_m]);
 //   MODE 2 (sample threshold): thr[q] = min(thr[q], the k-th smallest key)
 //     when there are at least k (run_merge's threshold-only level).
 // zero_count resets the count once every thread has read it.
@@ -554,20 +556,23 @@ __global__ void __launch_bounds__(kSelectThreads)
                   const uint64_t* __restrict__ keys, int64_t cap, uint32_t* __restrict__ count,
                   int zero_count, int k, int P2, uint64_t* __restrict__ thr,
                   float* __restrict__ out_dist, int64_t* __restrict__ out_row,
-                  const uint32_t* __restrict__ gate, int64_t gate_cap) {
+                  const uint64_t* __restrict__ alt, int64_t alt_m, int64_t alt_gate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   MergeShared* ms = reinterpret_cast<MergeShared*>(smem);
   uint64_t* res = reinterpret_cast<uint64_t*>(smem + sizeof(MergeShared));
   uint64_t* s = res + P2;
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t q = blockIdx.y;
-  if (gate != nullptr && (int64_t)gate[q * kCountStride] <= gate_cap) return;
   const uint32_t c = count[q * kCountStride];
-  const int64_t m = (int64_t)c < cap ? (int64_t)c : cap;
+  int64_t m = (int64_t)c < cap ? (int64_t)c : cap;
+  const uint64_t* src = keys + q * cap;
+  if (MODE == 1 && alt != nullptr && (int64_t)c > alt_gate) {
+    m = alt_m;
+    src = alt + q * alt_m;
+  }
   __syncthreads();
   if (zero_count && tid == 0) count[q * kCountStride] = 0u;
   if (MODE != 1 && m < k) return;  // (uniform) fewer than k candidates: no threshold
-  const uint64_t* src = keys + q * cap;
   int nres = 0;
   const int64_t chunk = kSelectEntries - k;
   for (int64_t off = 0; off < m || (off == 0 && m == 0); off += chunk) {  // (uniform)
@@ -673,8 +678,8 @@ template <typename T, int MODE>
 static int launch_select_t(const T* X, int64_t n, int d, int64_t row_base, const float* Q,
                            const float* qnorm, int64_t nq, const uint64_t* keys, int64_t cap,
                            uint32_t* count, int zero, int k, int metric, uint64_t* thr,
-                           float* out_dist, int64_t* out_row, const uint32_t* gate,
-                           int64_t gate_cap, hipStream_t stream) {
+                           float* out_dist, int64_t* out_row, const uint64_t* alt,
+                           int64_t alt_m, int64_t alt_gate, hipStream_t stream) {
   const void* fn = metric == FX_METRIC_COS  ? (const void*)select_kernel<T, 2, MODE>
                    : metric == FX_METRIC_IP ? (const void*)select_kernel<T, 1, MODE>
                                             : (const void*)select_kernel<T, 0, MODE>;
@@ -692,11 +697,11 @@ static int launch_select_t(const T* X, int64_t n, int d, int64_t row_base, const
     uint64_t* tq = thr != nullptr ? thr + q0 : nullptr;
     float* od = out_dist != nullptr ? out_dist + q0 * k : nullptr;
     int64_t* orow = out_row != nullptr ? out_row + q0 * k : nullptr;
-    const uint32_t* gq = gate != nullptr ? gate + q0 * kCountStride : nullptr;
-    void* args[] = {(void*)&x,   (void*)&n,   (void*)&d,    (void*)&row_base, (void*)&qv,
-                    (void*)&qnm, (void*)&kq,  (void*)&cap,  (void*)&cq,       (void*)&zero,
-                    (void*)&k,   (void*)&P2,  (void*)&tq,   (void*)&od,       (void*)&orow,
-                    (void*)&gq,  (void*)&gate_cap};
+    const uint64_t* aq = alt != nullptr ? alt + q0 * alt_m : nullptr;
+    void* args[] = {(void*)&x,   (void*)&n,   (void*)&d,     (void*)&row_base, (void*)&qv,
+                    (void*)&qnm, (void*)&kq,  (void*)&cap,   (void*)&cq,       (void*)&zero,
+                    (void*)&k,   (void*)&P2,  (void*)&tq,    (void*)&od,       (void*)&orow,
+                    (void*)&aq,  (void*)&alt_m, (void*)&alt_gate};
     hipError_t e = hipLaunchKernel(fn, dim3(1, (unsigned)qn), dim3(kSelectThreads), args, smem,
                                    stream);
     if (e != hipSuccess) {
@@ -718,10 +723,10 @@ int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t r
   if (dtype == FX_DTYPE_F16)
     return launch_select_t<_Float16, 0>(reinterpret_cast<const _Float16*>(X), n, d, row_base, Q,
                                         qnorm, nq, keys, cap, count, zero_count ? 1 : 0, k, metric,
-                                        thr, nullptr, nullptr, nullptr, 0, stream);
+                                        thr, nullptr, nullptr, nullptr, 0, 0, stream);
   return launch_select_t<float, 0>(reinterpret_cast<const float*>(X), n, d, row_base, Q, qnorm, nq,
                                    keys, cap, count, zero_count ? 1 : 0, k, metric, thr, nullptr,
-                                   nullptr, nullptr, 0, stream);
+                                   nullptr, nullptr, 0, 0, stream);
 }
 
 int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint32_t* count,
@@ -732,12 +737,12 @@ int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint3
   }
   return launch_select_t<float, 2>(nullptr, 0, 1, 0, nullptr, nullptr, nq, keys, cap, count,
                                    zero_count ? 1 : 0, k, FX_METRIC_L2, thr, nullptr, nullptr,
-                                   nullptr, 0, stream);
+                                   nullptr, 0, 0, stream);
 }
 
 int launch_final_select(const uint64_t* keys, int64_t nq, int64_t cap, const uint32_t* count,
-                        int k, float* out_dist, int64_t* out_row, const uint32_t* gate,
-                        int64_t gate_cap, hipStream_t stream) {
+                        int k, float* out_dist, int64_t* out_row, const uint64_t* alt,
+                        int64_t alt_m, int64_t alt_gate, hipStream_t stream) {
   if (k > kSelectEntries / 2) {
     set_error("final select: k %d too large", k);
     return FX_EUNSUPPORTED;
@@ -745,7 +750,7 @@ int launch_final_select(const uint64_t* keys, int64_t nq, int64_t cap, const uin
   // (MODE 1 reads no rows: the keys are exact composites already)
   return launch_select_t<float, 1>(nullptr, 0, 1, 0, nullptr, nullptr, nq, keys, cap,
                                    const_cast<uint32_t*>(count), 0, k, FX_METRIC_L2, nullptr,
-                                   out_dist, out_row, gate, gate_cap, stream);
+                                   out_dist, out_row, alt, alt_m, alt_gate, stream);
 }
 
 }  // namespace fx

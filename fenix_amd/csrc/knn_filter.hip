@@ -1360,9 +1360,11 @@ __device__ __forceinline__ void i3_epilogue(const f32x16 (&acc)[kI2QT], const fl
 // knn_batch.hip exact_distance16: dot and norms in f32, one division).  Each
 // per-query coefficient carries a relative slack >= 16 u (the roundings of the
 // products and sums of the test) and the test compares with 12582912 - 8.
-// The appends' [lb, ub] are evaluated in double from the same terms and
-// rounded outward.  A non-finite row or query, or one whose scaled norm
-// would exceed 2048, is forced through (omega or R' not finite).
+// The appends' [lb, ub] (i8_bounds) are evaluated in f32 from the same terms,
+// each widened outward by 16 u of the magnitudes it was computed from (every
+// rounding on the way is relative to a term it is added to, at most ~8 u).
+// A non-finite row or query, or one whose scaled norm would exceed 2048, is
+// forced through (omega or R' not finite).
 constexpr float kI8Magic = 12582912.f;   // 1.5 * 2^23: bits 0x4B400000
 constexpr float kI8C0 = 12582912.f - 8.f;
 
@@ -2098,15 +2100,29 @@ __global__ void __launch_bounds__(kI6Threads, 1) filter_img6_kernel(FilterArgs a
         __builtin_bit_cast(i32x4, xv), __builtin_bit_cast(i32x4, bv),
         __builtin_bit_cast(i32x16, cin), 0, 0, 0));
   };
-  // one k-step: its 4 B fragments first (one LDS wait), then the 4 MFMAs
+  // one k-step: its B fragments first (one LDS wait), then the MFMAs.  The
+  // previous k-step's fragments stay allocated until this k-step's reads are
+  // issued: an LDS read may return before an MFMA issued just ahead of it
+  // (waiting on the SIMD's matrix pipe behind the partner wave's MFMAs) has
+  // read its B operand, and the compiler, which sees the operand consumed at
+  // issue, would otherwise put the new fragments in those registers (seen as
+  // candidate counts moving by a few for query lanes 16-31 between identical
+  // runs, tools/race_check.py)
+  f16x8 bprev[kI2QT];
+#pragma unroll
+  for (int u = 0; u < kI2QT; ++u) bprev[u] = f16x8(0);
   auto kstep = [&](const f16x8& xv, int ks, bool start) {
     f16x8 bv[kI2QT];
 #pragma unroll
     for (int u = 0; u < kI2QT; ++u) bv[u] = bfrag(ks, u);
+#pragma unroll
+    for (int u = 0; u < kI2QT; ++u) asm volatile("" ::"v"(bprev[u]));
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < kI2QT; ++u) mfma(u, xv, bv[u], start);
     __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kI2QT; ++u) bprev[u] = bv[u];
   };
   const int lr = wid * 32 + l32;  // the wave's row this lane notes (lanes 0-31)
   int64_t ti = blockIdx.x;
@@ -3470,14 +3486,22 @@ bool filter_ring() { return diag_env("FX_FILTER_RING", 0) != 0; }
 // Batches of <= 64 queries take the 64-query tiles, 65..128 the 128-query ones
 // (their Qh is padded to 64 / 128, filter_query_pad)
 int launch_filter(const FilterArgs& a, int metric, hipStream_t stream) {
-  // int8 images: filter_img3_kernel with 64-, 128- or 256-query tiles
+  // int8 images: a batch that fits one resident slice (<= 128 queries) runs
+  // filter_img6_kernel (option "img6" 1; configs[1] 1.29 vs 1.34 ms, 128 L2
+  // queries 1.81 vs 1.93 ms), larger ones filter_img3_kernel with 256-query
+  // tiles (256 cosine queries: 2.97 ms against 3.34 ms for two img6 slices;
+  // option 2 forces the slices, 0 disables img6)
   if (a.img8) {
+    const int64_t i6 = option(kOptImg6);
     if (a.nq <= 64) {
-      if (option(kOptImg6) >= 2 && q64i::img6_fits(a.dq)) return q64i::launch_img6(a, metric, stream);
+      if (i6 >= 1 && q64i::img6_fits(a.dq)) return q64i::launch_img6(a, metric, stream);
       return q64i::launch(a, metric, stream);
     }
-    if (option(kOptImg6) != 0 && q128::img6_fits(a.dq)) return q128::launch_img6(a, metric, stream);
-    if (a.nq <= 128) return q128::launch(a, metric, stream);
+    if (a.nq <= 128) {
+      if (i6 >= 1 && q128::img6_fits(a.dq)) return q128::launch_img6(a, metric, stream);
+      return q128::launch(a, metric, stream);
+    }
+    if (i6 >= 2 && q128::img6_fits(a.dq)) return q128::launch_img6(a, metric, stream);
     return q256::launch(a, metric, stream);
   }
   if (a.nq <= 64) return q64::launch(a, metric, stream);

@@ -805,41 +805,42 @@ def test_single_query_through_filter_image(eng, metric, bits):
 
 @pytest.mark.parametrize("metric", METRICS)
 def test_img6_resident_slices_equal_streamed_tile(eng, metric):
-    """Int8-image batches of more than 64 queries run the resident-query-
-    slice kernel (option "img6": 128-query slices in LDS, slices of one batch
-    on CUs sharing the tiles); the same products, pass test and bounds as the
-    streamed-tile kernel, so the same candidate counts and results bit for
-    bit, equal to the exact scan -- across the 128 / 256 slice edges, with
-    rows the image cannot represent and with a mask."""
+    """Int8-image batches of up to 128 queries (single queries included) run
+    the resident-query-slice kernel (option "img6": 64- or 128-query slices
+    in LDS; with img6 = 2 larger batches too, their slices on CUs sharing the
+    tiles); the same products, pass test and bounds as the streamed-tile
+    kernel, so the same candidate counts and results bit for bit, equal to
+    the exact scan -- across the 64 / 128 / 256 slice edges, with rows the
+    image cannot represent and with a mask."""
     n, d, k = 70_000, 136, 30
     xh = _extreme_rows(n, d, 49)
     x = torch.from_numpy(xh).to(eng.device)
     eng.clear_images()
     mask = np.random.RandomState(4).rand(n) < 0.8
     m = _lib.METRICS[metric]
-    for nq in (65, 128, 129, 256, 300):
+    for nq in (1, 7, 64, 65, 128, 129, 256, 300):
         qh = O.fill_normal(nq, d, seed=60 + nq)
-        qh[3] = xh[17] * 2.0
+        qh[min(3, nq - 1)] = xh[17] * 2.0
         q = torch.from_numpy(qh).to(eng.device)
         for msk in (None, mask):
             dm = device_mask(msk, eng.device) if msk is not None else None
             got = {}
-            for img6 in (1, 0):
-                with _lib.options(img6=img6, filter_image=8):
+            for img6 in (2, 0):
+                with _lib.options(img6=img6, filter_image=8, batch_min_queries=1):
                     st = eng.scan(Shard(x, 0), q, m, k, dm)
                     counts, cap = eng.filter_counts(Shard(x, 0), nq, m, k, st)
                     od = torch.empty((nq, k), dtype=torch.float32, device=eng.device)
                     orow = torch.empty((nq, k), dtype=torch.int64, device=eng.device)
                     eng.reduce(Shard(x, 0), q, m, k, st, od, orow, dm)
                     got[img6] = (counts, od.cpu().numpy(), orow.cpu().numpy())
-            assert got[1][0] is not None
-            np.testing.assert_array_equal(got[1][0], got[0][0])
-            np.testing.assert_array_equal(got[1][2], got[0][2])
-            np.testing.assert_array_equal(got[1][1].view(np.uint32), got[0][1].view(np.uint32))
+            assert got[2][0] is not None
+            np.testing.assert_array_equal(got[2][0], got[0][0], err_msg=f"nq {nq} mask {msk is not None}")
+            np.testing.assert_array_equal(got[2][2], got[0][2])
+            np.testing.assert_array_equal(got[2][1].view(np.uint32), got[0][1].view(np.uint32))
             with _lib.options(batched=0):
                 sd, sr = gpu_search(eng, x, qh, metric, k, mask=msk)
-            np.testing.assert_array_equal(got[1][2], sr)
-            np.testing.assert_array_equal(got[1][1].view(np.uint32), sd.view(np.uint32))
+            np.testing.assert_array_equal(got[2][2], sr)
+            np.testing.assert_array_equal(got[2][1].view(np.uint32), sd.view(np.uint32))
     eng.clear_images()
 
 

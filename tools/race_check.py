@@ -1,0 +1,49 @@
+"""Determinism check of the int8 filter kernels: the same search repeated,
+per-query candidate counts compared across repetitions (a count that moves
+means a kernel read data that had not landed).  Prints one line per case.
+
+    python tools/race_check.py [--reps 30]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fenix_amd import _lib  # noqa: E402
+from fenix_amd.engine import Engine, Shard, device_mask  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+from tests.test_gpu_kernels import _extreme_rows  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--reps", type=int, default=30)
+a = p.parse_args()
+eng = Engine.get(torch.device("cuda", 0))
+k = 30
+for n, d in ((70_000, 136), (70_000, 768)):
+    xh = _extreme_rows(n, d, 49)
+    x = torch.from_numpy(xh).to(eng.device)
+    eng.clear_images()
+    mask = device_mask(np.random.RandomState(4).rand(n) < 0.8, eng.device)
+    for nq in (65, 256):
+        q = torch.from_numpy(O.fill_normal(nq, d, seed=60 + nq)).to(eng.device)
+        for msk in (None, mask):
+            for img6 in (0, 2):
+                with _lib.options(img6=img6, filter_image=8):
+                    ref = None
+                    moved = 0
+                    for _ in range(a.reps):
+                        st = eng.scan(Shard(x, 0), q, 0, k, msk)
+                        c, _cap = eng.filter_counts(Shard(x, 0), nq, 0, k, st)
+                        if ref is None:
+                            ref = c
+                        elif not np.array_equal(c, ref):
+                            moved += 1
+                            diff = np.nonzero(c != ref)[0]
+                            print(f"   d {d} nq {nq} mask {msk is not None} img6 {img6}: queries "
+                                  f"{diff[:20].tolist()} {(c[diff] - ref[diff])[:20].tolist()}",
+                                  flush=True)
+                    print(f"d {d} nq {nq} mask {msk is not None} img6 {img6}: {moved} of "
+                          f"{a.reps - 1} repetitions moved", flush=True)
