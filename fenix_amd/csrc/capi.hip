@@ -43,7 +43,7 @@ static const char* const kOptNames[kOptCount] = {
     "force_fallback", "scan_interleave", "q8_dma", "filter_image", "batch_ub_test",
     "single_query_image", "i8_max_k", "img6"};
 static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}, {8}, {1}, {1},
-                                                 {256}, {0}};
+                                                 {256}, {1}};
 
 int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
 

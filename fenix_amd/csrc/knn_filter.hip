@@ -2002,7 +2002,7 @@ static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
 // alone: its own 32-row tiles, FX_I6_XS image k-steps in flight in registers
 // across tile ends, its own rows' terms and flags in LDS, the same epilogue
 // (i8_epilogue: pass test, bounds, LDS append segments shared through LDS
-// atomics).  No barrier between the prologue and the final segment flush.
+// atomics).  One barrier per tile, before the epilogue (see there).
 // A batch of more than 128 queries runs its slices on different CUs over
 // the same tiles at the same time -- workgroup (x, y) takes slice y and
 // tiles x, x + G, ... with G = CUs / slices, so the partners share an XCD
@@ -2102,12 +2102,9 @@ __global__ void __launch_bounds__(kI6Threads, 1) filter_img6_kernel(FilterArgs a
   };
   // one k-step: its B fragments first (one LDS wait), then the MFMAs.  The
   // previous k-step's fragments stay allocated until this k-step's reads are
-  // issued: an LDS read may return before an MFMA issued just ahead of it
-  // (waiting on the SIMD's matrix pipe behind the partner wave's MFMAs) has
-  // read its B operand, and the compiler, which sees the operand consumed at
-  // issue, would otherwise put the new fragments in those registers (seen as
-  // candidate counts moving by a few for query lanes 16-31 between identical
-  // runs, tools/race_check.py)
+  // issued, so the new fragments never land in registers an MFMA issued just
+  // ahead (and possibly still queued behind the partner wave's MFMAs) reads
+  // (defensive: the measured hazard was the epilogue's, below)
   f16x8 bprev[kI2QT];
 #pragma unroll
   for (int u = 0; u < kI2QT; ++u) bprev[u] = f16x8(0);
@@ -2160,7 +2157,16 @@ __global__ void __launch_bounds__(kI6Threads, 1) filter_img6_kernel(FilterArgs a
       i8_note_row(sh->rinfo, sh->rterm, sh->rext, sh->rflags, lr, rsum[0], y1, rsum[1], ok);
       sh->rrow[lr] = (uint32_t)a.row_base + crow;
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // Every wave of the workgroup past its last MFMA before any epilogue
+    // reads its accumulators.  Without this barrier the waves ran free and
+    // the epilogue now and then read a product of the tile's last k-step
+    // before the MFMA had written it: the same search repeated appended one
+    // more or one fewer row for query lanes 16-31 of a tile (no padding of
+    // s_nop after the MFMAs removed it, so the MFMA was still queued behind
+    // the partner wave's on the SIMD's matrix pipe).  tools/race_check.py:
+    // 0 of 88 repetitions move with it, 201 of 232 without; it costs
+    // nothing on a single query (1.295 vs 1.300 ms for configs[1]).
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (!(diag & 2))
       i8_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rext, sh->rrow, sh->rflags, sh->qtab,
                           sh->qinf, a, q0, wid, h, l32, sh->seg, diag);

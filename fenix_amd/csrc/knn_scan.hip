@@ -875,9 +875,16 @@ int plan_scan(int64_t n, int64_t d, int dtype, int64_t k, int metric, bool align
   if (cap_occ > 0 && cap_occ < occ) occ = cap_occ;
   if (occ < 1) occ = 1;
   const int64_t max_blocks = (int64_t)cus * occ;
-  // each wave should see many more rows than k for the threshold to filter
+  // at least 2 k rows per block (k / 2 per wave): fewer rows than that and
+  // the lists outweigh the rows; more (8 k, before round 4) left most CUs
+  // idle on small shards at large k -- 500k x 1536 fp16, k = 1000: 62 blocks,
+  // 0.78 ms; 245 blocks, 0.33 ms (6.25M rows and k = 100 unchanged,
+  // profiles/r04_scan_min_rows.jsonl)
+#ifndef FX_SCAN_MIN_ROWS_K
+#define FX_SCAN_MIN_ROWS_K 2
+#endif
   int64_t min_rows = 16 * U * 4;
-  if (min_rows < 8 * k) min_rows = 8 * k;
+  if (min_rows < FX_SCAN_MIN_ROWS_K * k) min_rows = FX_SCAN_MIN_ROWS_K * k;
   if (min_rows < 256) min_rows = 256;
   int64_t blocks = (n + min_rows - 1) / min_rows;
   if (blocks > max_blocks) blocks = max_blocks;

@@ -89,7 +89,7 @@ int fx_device_count(int* out);
  *                            an int8 filter image is supplied
  *   "i8_max_k"          256  largest k an int8 filter image serves (larger k:
  *                            the fp16 image / f32 rows, or the exact scan)
- *   "img6"                0  1: int8-image batches of <= 128 queries (single
+ *   "img6"                1  1: int8-image batches of <= 128 queries (single
  *                            queries included) run the resident-query-slice
  *                            kernel; 2: larger batches too (as several
  *                            slices); 0: every batch the streamed-query-tile

@@ -36,7 +36,7 @@ def run(img6):
                                          st.ws.numel(), thr.data_ptr(), cand.data_ptr(),
                                          cub.data_ptr(), torch.cuda.current_stream().cuda_stream))
         torch.cuda.synchronize()
-        return counts, thr.cpu().numpy(), cand.cpu().numpy().view(np.uint64), cap
+        return counts, thr.cpu().numpy(), cub.cpu().numpy().view(np.uint64), cap
 
 
 def rows_of(res, i):
@@ -59,6 +59,16 @@ for r in range(len(runs)):
         only3 = sorted(set(b) - set(a))
         dif = [(rw, a[rw], b[rw]) for rw in set(a) & set(b) if a[rw] != b[rw]][:5]
         print(f"   q{i}: only img6 {only6[:6]} only img3 {only3[:6]} same row, other key {dif}")
+        lst = rows_of(runs[r], i)
+        rws = (lst & np.uint64(0xffffffff)).astype(np.int64)
+        u, cnt = np.unique(rws, return_counts=True)
+        dup = u[cnt > 1]
+        for rw in dup[:3]:
+            slots = np.nonzero(rws == rw)[0]
+            print(f"      duplicate row {rw} at slots {slots.tolist()} of {len(lst)}, keys "
+                  f"{[hex(int(lst[s_] >> 32)) for s_ in slots]}; image row "
+                  f"{int((rw * pow(int(perm_a), -1, n)) % n)}")
+        ub = runs[r][2]
         for rw in (only6 + only3)[:4]:
             # image position of corpus row rw: i with (a i) mod n == rw
             pos = None
