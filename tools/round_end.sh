@@ -5,7 +5,7 @@
 # library's SHA (copied to gpurun_out/ so they come back), then the bench
 # lines again with the traffic fields filled in.  Every GPU step has its own
 # limit; a crash, abort or timeout ends the script.
-#   bash tools/round_end.sh ROUND [--no-tests]
+#   bash tools/round_end.sh ROUND [--no-tests | --tests-only]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=$(printf "%02d" "${1:-4}")
 mkdir -p gpurun_out/re
@@ -25,6 +25,7 @@ if [ "$2" != "--no-tests" ]; then
   run tests 1300 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread
   run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 fi
+[ "$2" == "--tests-only" ] && { echo "== done"; exit 0; }
 run bench1 300 python -u bench.py
 run bench2 300 python -u bench.py $CFG2 --no-cpu-baseline
 # the headline's kernel alone (exact fused scan; no filter-image leg, whose
