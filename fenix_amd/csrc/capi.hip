@@ -642,8 +642,11 @@ static int filter_phases(const BatchLayout& b, const void* X, int dtype, const v
 //     read once by F1 or F2 (the sampling phases re-read 1/r1 (1/r2 + ...)
 //     of them);
 //   the exact k-th of all candidates' k best upper bounds is the final
-//     threshold, and the candidates whose lower bound reaches it are
+//     threshold (batches of more than kI8RescoreAllMaxQ queries; smaller ones
+//     keep F1's), and the candidates whose lower bound reaches it are
 //     rescored exactly (launch_rescore), fx_knn_reduce selects the top k.
+static constexpr int64_t kI8RescoreAllMaxQ = 2;
+
 static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, const void* image,
                             const float* rowinfo, int64_t n, int64_t d, int64_t row_base,
                             const float* Q, int64_t nq, int metric, int64_t k,
@@ -730,8 +733,13 @@ static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, cons
       if (rc) return rc;
     }
   }
-  rc = exact_threshold(cand_ub, false);
-  if (rc) return rc;
+  // the final threshold only pays for itself on a batch: one or two queries
+  // rescore every candidate under F1's threshold instead (a few thousand 3 KB
+  // rows, ~3-6 us spread over the chip, against a ~25 us one-workgroup select)
+  if (m < 2 || nq > kI8RescoreAllMaxQ) {
+    rc = exact_threshold(cand_ub, false);
+    if (rc) return rc;
+  }
   return launch_rescore(X, dtype, n, (int)d, row_base, Q, qnorm, nq, count, cand, (int)b.cap,
                         metric, thr, st);
 }

@@ -357,6 +357,42 @@ __device__ __forceinline__ float exact_distance16(const T* __restrict__ xr,
 // unread.  Each wave takes 64 slots at a time, one per lane, and rescores the
 // kept ones 4 at a time (a 16-lane group each, the kept lanes taken in order
 // from the wave's ballot): dropped candidates cost one load and no group.
+// Small query counts (kRescoreDenseMaxQ), whose candidates are mostly kept:
+// every 16-lane group takes its own slot (4 per wave per step), so a few
+// thousand candidates cost one round trip each across the whole grid
+// instead of up to 16 rounds per wave (single query, 3.3 K candidates: ~25
+// -> a few us).
+constexpr unsigned kRescoreDenseMaxQ = 2;
+template <typename T, int METRIC>
+__global__ void __launch_bounds__(256) rescore_dense_kernel(const T* __restrict__ X, int64_t n,
+                                                            int d, int64_t row_base,
+                                                            const float* __restrict__ Q,
+                                                            const float* __restrict__ qnorm,
+                                                            const uint32_t* __restrict__ count,
+                                                            uint64_t* __restrict__ cand, int cap,
+                                                            const uint64_t* __restrict__ thr) {
+  const int64_t q = blockIdx.y;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int grp = lane >> 4, jl = lane & 15;
+  const uint32_t cq = count[q * kCountStride];
+  const int64_t cnt = cq < (uint32_t)cap ? cq : (uint32_t)cap;
+  const uint32_t tkey = thr != nullptr ? (uint32_t)(thr[q] >> 32) : 0xffffffffu;
+  const float* qv = Q + q * (int64_t)d;
+  const float qn = METRIC == 2 ? qnorm[q] : 0.f;
+  uint64_t* cl = cand + q * (int64_t)cap;
+  for (int64_t base = ((int64_t)blockIdx.x * 4 + wv) * 4; base < cnt;
+       base += (int64_t)gridDim.x * 16) {  // wave-uniform trip count
+    const int64_t i = base + grp;
+    const uint64_t c = i < cnt ? cl[i] : kEmpty;
+    const int64_t row = (int64_t)(c & 0xffffffffull) - row_base;
+    const bool keep = c != kEmpty && (uint32_t)(c >> 32) <= tkey && row >= 0 && row < n;
+    const float dist =
+        exact_distance16<T, METRIC>(X + (keep ? row : 0) * (int64_t)d, qv, d, jl, keep, qn);
+    if (jl == 0 && c != kEmpty)
+      cl[i] = keep ? make_comp(dist, (uint32_t)(c & 0xffffffffull)) : kEmpty;
+  }
+}
+
 template <typename T, int METRIC>
 __global__ void __launch_bounds__(256) rescore_kernel(const T* __restrict__ X, int64_t n, int d,
                                                       int64_t row_base,
@@ -451,6 +487,23 @@ template <typename T>
 static void launch_rescore_t(const T* X, int64_t n, int d, int64_t row_base, const float* Q,
                              const float* qnm, const uint32_t* count, uint64_t* cand, int cap,
                              int metric, const uint64_t* t, dim3 grid, hipStream_t stream) {
+  if (grid.y <= kRescoreDenseMaxQ) {
+    // (one slot per 16-lane group: 16 K slots per grid step, fewer blocks
+    // when the buffer is smaller)
+    dim3 g2 = grid;
+    const int64_t need = ((int64_t)cap + 15) / 16;
+    g2.x = (unsigned)(need < 1024 ? need : 1024);
+    if (metric == FX_METRIC_COS)
+      hipLaunchKernelGGL((rescore_dense_kernel<T, 2>), g2, dim3(256), 0, stream, X, n, d,
+                         row_base, Q, qnm, count, cand, cap, t);
+    else if (metric == FX_METRIC_IP)
+      hipLaunchKernelGGL((rescore_dense_kernel<T, 1>), g2, dim3(256), 0, stream, X, n, d,
+                         row_base, Q, qnm, count, cand, cap, t);
+    else
+      hipLaunchKernelGGL((rescore_dense_kernel<T, 0>), g2, dim3(256), 0, stream, X, n, d,
+                         row_base, Q, qnm, count, cand, cap, t);
+    return;
+  }
   if (metric == FX_METRIC_COS) {
     hipLaunchKernelGGL((rescore_kernel<T, 2>), grid, dim3(256), 0, stream, X, n, d, row_base, Q,
                        qnm, count, cand, cap, t);

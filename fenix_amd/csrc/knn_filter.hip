@@ -2016,6 +2016,7 @@ constexpr int kI6Threads = 64 * kI6Waves;
 constexpr int kI6BM = 32 * kI6Waves;
 static_assert(kI6BM == fBM, "one plan tile per workgroup tile");
 constexpr int kI6SEG = FX_I3_SEG;
+constexpr int kI6SliceBatch = 12;  // 768-d, 128 queries: every piece of the slice in one batch
 struct Img6Shared {
   float rinfo[kI6BM];
   float rterm[kI6BM];
@@ -2055,13 +2056,28 @@ __global__ void __launch_bounds__(kI6Threads, 1) filter_img6_kernel(FilterArgs a
   i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, kI6Threads);
   for (int q = tid; q < fBQ; q += kI6Threads) sh->seg[q] = 0u;
   {  // the slice: chunk c of query Q at (c * 128 + Q) * 64, piece p at (p ^ ((Q >> 2) & 3)) * 16
-    const int nch = a.dq / 64;
+    // (kI6SliceBatch loads in flight per thread before their stores: one
+    // load, wait, store per iteration cost ~1.5 us each, ~18 us per launch)
+    const int total = a.dq / 64 * fBQ * 4;
     const unsigned char* qb = reinterpret_cast<const unsigned char*>(a.Qh);
-    for (int i = tid; i < nch * fBQ * 4; i += kI6Threads) {
-      const int c = i / (fBQ * 4), Q = (i / 4) % fBQ, pc = i % 4;
-      const i32x4 v = *reinterpret_cast<const i32x4*>(
-          qb + ((int64_t)c * a.qstride + q0 + Q) * 64 + pc * 16);
-      *reinterpret_cast<i32x4*>(qslice + ((c * fBQ + Q) * 64 + ((pc ^ ((Q >> 2) & 3)) * 16))) = v;
+    for (int i0 = tid; i0 < total; i0 += kI6SliceBatch * kI6Threads) {
+      i32x4 v[kI6SliceBatch];
+#pragma unroll
+      for (int j = 0; j < kI6SliceBatch; ++j) {
+        const int i = i0 + j * kI6Threads;
+        const int c = i / (fBQ * 4), Q = (i / 4) % fBQ, pc = i % 4;
+        if (i < total)
+          v[j] = *reinterpret_cast<const i32x4*>(qb + ((int64_t)c * a.qstride + q0 + Q) * 64 +
+                                                 pc * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < kI6SliceBatch; ++j) {
+        const int i = i0 + j * kI6Threads;
+        const int c = i / (fBQ * 4), Q = (i / 4) % fBQ, pc = i % 4;
+        if (i < total)
+          *reinterpret_cast<i32x4*>(qslice + ((c * fBQ + Q) * 64 + ((pc ^ ((Q >> 2) & 3)) * 16))) =
+              v[j];
+      }
     }
   }
   __syncthreads();
