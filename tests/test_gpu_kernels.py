@@ -844,6 +844,31 @@ def test_img6_resident_slices_equal_streamed_tile(eng, metric):
     eng.clear_images()
 
 
+@pytest.mark.parametrize("img6", [0, 2])
+def test_filter_candidate_counts_repeat_exactly(eng, img6):
+    """The same int8-image search repeated appends exactly the same
+    candidates: a kernel that reads a product, a query chunk or a row term
+    before it has landed shows up as counts moving between identical runs
+    long before it moves a result (tools/race_check.py; the resident-slice
+    kernel without its pre-epilogue barrier moved in 201 of 232 repetitions,
+    DESIGN.md 3.6d item 7)."""
+    n, d, k = 70_000, 768, 30
+    x = torch.from_numpy(_extreme_rows(n, d, 49)).to(eng.device)
+    eng.clear_images()
+    for nq in (65, 256):
+        q = torch.from_numpy(O.fill_normal(nq, d, seed=60 + nq)).to(eng.device)
+        with _lib.options(img6=img6, filter_image=8):
+            ref = None
+            for _ in range(8):
+                st = eng.scan(Shard(x, 0), q, _lib.METRICS["l2"], k)
+                c, _cap = eng.filter_counts(Shard(x, 0), nq, _lib.METRICS["l2"], k, st)
+                assert c is not None
+                if ref is None:
+                    ref = c
+                np.testing.assert_array_equal(c, ref, err_msg=f"nq {nq}: counts moved")
+    eng.clear_images()
+
+
 def test_filter_image_follows_corpus_changes(eng):
     """The cached image is keyed on the corpus tensor's version: an in-place
     torch update and a rewrite through Engine.fill both rebuild it, so the

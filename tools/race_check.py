@@ -19,9 +19,35 @@ from tests.test_gpu_kernels import _extreme_rows  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument("--reps", type=int, default=30)
+p.add_argument("--fp16", action="store_true",
+               help="the fp16 filter kernels instead: fp16 image (k = 30) and no image (k = 300)")
 a = p.parse_args()
 eng = Engine.get(torch.device("cuda", 0))
 k = 30
+if a.fp16:
+    for n, d in ((70_000, 136), (70_000, 768)):
+        xh = _extreme_rows(n, d, 49)
+        x = torch.from_numpy(xh).to(eng.device)
+        for nq in (65, 256):
+            q = torch.from_numpy(O.fill_normal(nq, d, seed=60 + nq)).to(eng.device)
+            for name, opts, kk in (("fp16 image", {"filter_image": 16}, 30),
+                                   ("no image", {"filter_image": 0}, 300)):
+                eng.clear_images()
+                with _lib.options(**opts):
+                    ref, moved = None, 0
+                    for _ in range(a.reps):
+                        st = eng.scan(Shard(x, 0), q, 0, kk)
+                        c, _cap = eng.filter_counts(Shard(x, 0), nq, 0, kk, st)
+                        if c is None:
+                            break
+                        if ref is None:
+                            ref = c
+                        elif not np.array_equal(c, ref):
+                            moved += 1
+                    print(f"d {d} nq {nq} {name} k {kk}: "
+                          + ("no filter" if ref is None else
+                             f"{moved} of {a.reps - 1} repetitions moved"), flush=True)
+    sys.exit(0)
 for n, d in ((70_000, 136), (70_000, 768)):
     xh = _extreme_rows(n, d, 49)
     x = torch.from_numpy(xh).to(eng.device)
