@@ -600,7 +600,10 @@ int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_bas
 //   MODE 2 (sample threshold): thr[q] = min(thr[q], the k-th smallest key)
 //     when there are at least k (run_merge's threshold-only level).
 // zero_count resets the count once every thread has read it.
-constexpr int kSelectThreads = 1024;
+#ifndef FX_SELECT_THREADS
+#define FX_SELECT_THREADS 1024
+#endif
+constexpr int kSelectThreads = FX_SELECT_THREADS;
 constexpr int kSelectEntries = 16384;  // LDS chunk (128 KB)
 template <typename T, int METRIC, int MODE>
 __global__ void __launch_bounds__(kSelectThreads)
