@@ -818,7 +818,7 @@ def test_img6_resident_slices_equal_streamed_tile(eng, metric):
     eng.clear_images()
     mask = np.random.RandomState(4).rand(n) < 0.8
     m = _lib.METRICS[metric]
-    for nq in (1, 7, 64, 65, 128, 129, 256, 300):
+    for nq in (1, 2, 3, 7, 64, 65, 128, 129, 256, 300):
         qh = O.fill_normal(nq, d, seed=60 + nq)
         qh[min(3, nq - 1)] = xh[17] * 2.0
         q = torch.from_numpy(qh).to(eng.device)
@@ -841,6 +841,35 @@ def test_img6_resident_slices_equal_streamed_tile(eng, metric):
                 sd, sr = gpu_search(eng, x, qh, metric, k, mask=msk)
             np.testing.assert_array_equal(got[2][2], sr)
             np.testing.assert_array_equal(got[2][1].view(np.uint32), sd.view(np.uint32))
+    eng.clear_images()
+
+
+@pytest.mark.parametrize("metric", METRICS)
+def test_small_batches_rescore_all_and_fallback_lists(eng, metric):
+    """One or two queries through the int8 image skip the final exact
+    threshold and rescore every candidate under F1's (rescore_dense_kernel);
+    an overflowing query's exact-scan lists feed the final select directly
+    (no merge levels).  With a mask, forced through the fallback or not, the
+    results equal the exact scan bit for bit, at 1, 2 and 3 queries (either
+    side of both switches)."""
+    n, d, k = 90_000, 192, 50
+    xh = _extreme_rows(n, d, 71)
+    x = torch.from_numpy(xh).to(eng.device)
+    eng.clear_images()
+    mask = np.random.RandomState(72).rand(n) < 0.7
+    for nq in (1, 2, 3):
+        qh = O.fill_normal(nq, d, seed=73 + nq)
+        for msk in (None, mask):
+            with _lib.options(batched=0):
+                sd, sr = gpu_search(eng, x, qh, metric, k, mask=msk)
+            with _lib.options(batch_min_queries=1, filter_image=8):
+                assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, nq, k, _lib.METRICS[metric])
+                fd, fr = gpu_search(eng, x, qh, metric, k, mask=msk)
+                with _lib.options(force_fallback=1):
+                    gd, gr = gpu_search(eng, x, qh, metric, k, mask=msk)
+            for dd, rr in ((fd, fr), (gd, gr)):
+                np.testing.assert_array_equal(rr, sr)
+                np.testing.assert_array_equal(dd.view(np.uint32), sd.view(np.uint32))
     eng.clear_images()
 
 
