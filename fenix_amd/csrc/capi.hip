@@ -454,12 +454,11 @@ static int plan_search(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, i
 }
 
 
-// The fallback's gated scan alone over all nq queries (s.fb_queries >= nq):
-// per overflowing query nlists lists of k composites at *lists, [nq][nlists k]
-static int fallback_scan(const SearchLayout& s, const void* corpus, int64_t n, int64_t d,
-                         int64_t row_base, const float* queries, int64_t nq, int64_t k,
-                         const uint32_t* mask, const uint32_t* count, int64_t gate_cap, char* ws,
-                         hipStream_t st, const uint64_t** lists) {
+// The fallback scan's arguments: top-k lists into ws, each workgroup gated
+// on its query's count (> gate_cap: recompute)
+static ScanArgs fallback_args(const SearchLayout& s, const void* corpus, int64_t n, int64_t d,
+                              int64_t row_base, int64_t k, const uint32_t* mask, int64_t gate_cap,
+                              char* ws) {
   ScanArgs a = {};
   a.X = corpus;
   a.n = n;
@@ -473,6 +472,16 @@ static int fallback_scan(const SearchLayout& s, const void* corpus, int64_t n, i
   a.mode = kModeTopk;
   a.out_lists = reinterpret_cast<uint64_t*>(ws);
   a.gate_cap = gate_cap;
+  return a;
+}
+
+// The fallback's gated scan alone over all nq queries (s.fb_queries >= nq):
+// per overflowing query nlists lists of k composites at *lists, [nq][nlists k]
+static int fallback_scan(const SearchLayout& s, const void* corpus, int64_t n, int64_t d,
+                         int64_t row_base, const float* queries, int64_t nq, int64_t k,
+                         const uint32_t* mask, const uint32_t* count, int64_t gate_cap, char* ws,
+                         hipStream_t st, const uint64_t** lists) {
+  ScanArgs a = fallback_args(s, corpus, n, d, row_base, k, mask, gate_cap, ws);
   a.q = queries;
   a.gate = count;
   *lists = a.out_lists;
@@ -492,19 +501,7 @@ static int fallback_search(const SearchLayout& s, const void* corpus, int dtype,
                            hipStream_t st) {
   (void)dtype;
   (void)metric;
-  ScanArgs a = {};
-  a.X = corpus;
-  a.n = n;
-  a.d = (int)d;
-  a.row_base = row_base;
-  a.mask = mask;
-  a.rows_per_block = s.scan.rows_per_block;
-  a.k = (int)k;
-  a.cap = s.scan.cap;
-  a.qbytes = s.scan.qbytes;
-  a.mode = kModeTopk;
-  a.out_lists = reinterpret_cast<uint64_t*>(ws);
-  a.gate_cap = gate_cap;
+  ScanArgs a = fallback_args(s, corpus, n, d, row_base, k, mask, gate_cap, ws);
   for (int64_t q0 = 0; q0 < nq; q0 += s.fb_queries) {
     const int64_t qn = (nq - q0) < s.fb_queries ? (nq - q0) : s.fb_queries;
     a.q = queries + (size_t)q0 * d;
