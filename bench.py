@@ -570,6 +570,9 @@ def batch_leg(eng, shard, image, img_bytes, n, d, k, args, nb=256, mname="cosine
             sd.cpu().numpy().view(np.uint32), bd[idx].cpu().numpy().view(np.uint32)))
         assert same, "configs[2] batch differs from the exact scan"
     pass_bytes = img_bytes + nb * d * 4
+    # HBM bytes per search from the SHA-matched counter pass of the same
+    # workload (bench.py --nq 256 --metric cosine, tools/round_end.sh)
+    traffic = pmc_traffic(f"{n}x{d}_f32_{mname}_k{k}_q{nb}", "filter_img", _lib.library_sha())
     return {
         "workload": f"{n}x{d} f32 {mname} kNN k={k}, {nb}-query batch (query seed 2), "
                     "same shard and filter image",
@@ -582,6 +585,8 @@ def batch_leg(eng, shard, image, img_bytes, n, d, k, args, nb=256, mname="cosine
         "frac_over_image": pass_bytes / (span * 1e-3) / 1e9 / HBM_PEAK_GBS,
         "mfma_tflops": 2.0 * n * nb * d / (span * 1e-3) / 1e12,
         "mfma_peak_tflops": MFMA_F16_PEAK_TFS * 2,
+        "traffic": traffic,
+        "traffic_over_image": (traffic / pass_bytes) if traffic else None,
         "sample_bit_identical": same,
     }
 
