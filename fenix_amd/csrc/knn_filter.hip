@@ -1997,17 +1997,19 @@ static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
 // (as many bytes per chunk as the image itself) behind a workgroup barrier,
 // so the 8 waves run in lockstep and the MFMAs add to the image stream
 // instead of hiding under it.  Here a workgroup holds its
-// slice of 128 queries (the q128 build; 64 in q64i) in LDS for the whole kernel (96 KB at 768-d,
-// XOR-swizzled for conflict-free ds_read_b128) and each of its waves runs
-// alone: its own 32-row tiles, FX_I6_XS image k-steps in flight in registers
-// across tile ends, its own rows' terms and flags in LDS, the same epilogue
-// (i8_epilogue: pass test, bounds, LDS append segments shared through LDS
-// atomics).  One barrier per tile, before the epilogue (see there).
-// A batch of more than 128 queries runs its slices on different CUs over
-// the same tiles at the same time -- workgroup (x, y) takes slice y and
-// tiles x, x + G, ... with G = CUs / slices, so the partners share an XCD
-// (x + G y = x mod 8) and the second read of a tile can come from its L2 or
-// the Infinity Cache instead of HBM.
+// slice of 128 queries (the q128 build; 64 in q64i) in LDS for the whole
+// kernel (96 KB at 768-d, XOR-swizzled for conflict-free ds_read_b128) and
+// each of its waves runs its own 32-row tiles with FX_I6_XS image k-steps in
+// flight in registers across tile ends, its own rows' terms and flags in
+// LDS, and the same epilogue (i8_epilogue: pass test, bounds, LDS append
+// segments shared through LDS atomics); the only barrier of the tile loop
+// is the one before the epilogue (see there).  Default for batches of up to
+// 128 queries (launch_filter).  With option img6 = 2 a larger batch runs its
+// slices on different CUs over the same tiles at the same time --
+// workgroup (x, y) takes slice y and tiles x, x + G, ... with G = CUs /
+// slices, so the partners share an XCD (x + G y = x mod 8) and the second
+// read of a tile can come from its L2 or the Infinity Cache; measured slower
+// than filter_img3_kernel's 256-query tiles (3.34 vs 2.97 ms), so off.
 #ifndef FX_I6_XS
 #define FX_I6_XS 8
 #endif
