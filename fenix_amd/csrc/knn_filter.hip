@@ -2121,8 +2121,13 @@ __global__ void __launch_bounds__(kI6Threads, 1) filter_img6_kernel(FilterArgs a
   // one k-step: its B fragments first (one LDS wait), then the MFMAs.  The
   // previous k-step's fragments stay allocated until this k-step's reads are
   // issued, so the new fragments never land in registers an MFMA issued just
-  // ahead (and possibly still queued behind the partner wave's MFMAs) reads
-  // (defensive: the measured hazard was the epilogue's, below)
+  // ahead (and possibly still queued behind the partner wave's MFMAs) reads.
+  // Defensive only: the measured hazard was the epilogue's (below); without
+  // this (FX_I6_BPREV=0) 0 of 88 repetitions moved and the times were equal
+  // (profiles/r04_img6_bprev_sweep.jsonl)
+#ifndef FX_I6_BPREV
+#define FX_I6_BPREV 1
+#endif
   f16x8 bprev[kI2QT];
 #pragma unroll
   for (int u = 0; u < kI2QT; ++u) bprev[u] = f16x8(0);
@@ -2130,8 +2135,10 @@ __global__ void __launch_bounds__(kI6Threads, 1) filter_img6_kernel(FilterArgs a
     f16x8 bv[kI2QT];
 #pragma unroll
     for (int u = 0; u < kI2QT; ++u) bv[u] = bfrag(ks, u);
+    if constexpr (FX_I6_BPREV != 0) {
 #pragma unroll
-    for (int u = 0; u < kI2QT; ++u) asm volatile("" ::"v"(bprev[u]));
+      for (int u = 0; u < kI2QT; ++u) asm volatile("" ::"v"(bprev[u]));
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < kI2QT; ++u) mfma(u, xv, bv[u], start);
