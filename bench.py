@@ -19,7 +19,13 @@ configs[2]) run the product path in the headline, priced over the image bytes
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rows ROWS] [--d D]
                     [--k K] [--nq Q] [--metric l2|cosine|inner_product]
                     [--dtype f32|f16|qu8] [--cluster C] [--query normal|near]
-                    [--no-accelerated] [--no-cpu-baseline]
+                    [--no-accelerated] [--no-cpu-baseline] [--strong-rows R]
+                    [--serve-devices 0,1,...]
+
+For N > 1 the line also carries ``strong`` (BASELINE's fixed 10M-row corpus
+split over the N ranks) and ``serve`` (rank 0 alone: one process searching a
+row shard on every device through engine._search_all, the path a Flight
+server runs, with the RCCL all-gather and with peer copies).
 
 Every leg checks its result: sorted and complete, one planted row per rank
 returned first in rank order (global row numbering), for N > 1 the merge
@@ -36,6 +42,7 @@ Prints ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
 from __future__ import annotations
 
 import argparse
+import datetime
 import glob
 import json
 import os
@@ -83,7 +90,23 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                    help="library option (fx_set_option), e.g. batch_sample_ratio=20; sweeps only")
+    p.add_argument("--strong-rows", type=int, default=-1,
+                   help="N > 1: also time the exact search of this many rows in total, split "
+                        "over the N ranks (strong scaling; default --rows, i.e. configs[1]'s "
+                        "10M); 0 skips it")
+    p.add_argument("--serve-devices", default="",
+                   help="comma-separated ordinals: also time one process searching row shards "
+                        "on these devices (engine._search_all, the Flight server's path); "
+                        "default at N > 1: every rank's device, from rank 0")
     return p.parse_args()
+
+
+def check_frac(name: str, frac: float) -> float:
+    """A roofline fraction above 1 means the timed span did not bracket the
+    work it is priced on: fail loudly instead of printing it."""
+    if not frac <= 1.0:
+        sys.exit(f"bench.py: {name} = {frac:.3f} > 1: the timed span misses part of the work")
+    return frac
 
 
 def cpu_baseline(args):
@@ -230,6 +253,8 @@ def host_merge(gd: np.ndarray, gr: np.ndarray, k: int):
 
 def main():
     args = parse()
+    if args.strong_rows < 0:
+        args.strong_rows = args.n
     if args.gpus < 1:
         sys.exit("--gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -256,7 +281,7 @@ def main():
             dist.init_process_group("nccl", device_id=device)
 
     from fenix_amd import _lib
-    from fenix_amd.distributed import allgather_topk
+    from fenix_amd.distributed import allgather_topk, shard_rows
     from fenix_amd.engine import Engine, Shard
 
     eng = Engine.get(device)
@@ -288,39 +313,56 @@ def main():
     if not qu8 and not args.no_verify:
         planted = plant_rows(x, q, args.metric, rank, world)
         torch.autograd.graph.increment_version(x)
+
+    def planted_global(g, per_rank=None):
+        """Global row of rank g's planted row: rank g holds rows [g n, g n + n)
+        (weak scaling), or shard_rows(strong_rows, world, g) (strong)."""
+        p = (g * 7919 + 12345) % n
+        if per_rank is None:
+            return g * n + p
+        return shard_rows(per_rank, world, g)[0] + p
     shard = Shard(x, row_base, QU8_SCALE, QU8_ZP) if qu8 else Shard(x, row_base)
     od = torch.empty((nq, k), dtype=torch.float32, device=device)
     orow = torch.empty((nq, k), dtype=torch.int64, device=device)
 
-    def step(ev=None):
-        """One search of this rank's shard (+ the all-gather and final merge
-        for N > 1); ``ev``: HIP events bracketing the scan launches on the
-        stream they are queued on."""
-        if ev is not None:
-            ev[0].record()
-        if qu8:  # fx_knn_search_ex: scan + merge in one call (the merge is ~1 % of it)
-            with eng.lock:
-                eng.search_shard(shard, q, metric, k, None, od, orow)
-        else:
-            st = eng.scan(shard, q, metric, k)
-        if ev is not None:
-            ev[1].record()
-        if not qu8:
-            eng.reduce(shard, q, metric, k, st, od, orow)
-        if use_dist:
-            if gloo:
-                gd, gr = allgather_topk(od.cpu(), orow.cpu())
-                gd, gr = gd.to(device), gr.to(device)
-            else:
-                gd, gr = allgather_topk(od, orow)  # one RCCL all-gather over xGMI
-            md, mr = eng.merge(gd, gr, k)
-            return md, mr, gd, gr
-        return od.clone(), orow.clone(), None, None
+    def make_step(sh, span):
+        """One search of shard ``sh`` (+ the all-gather and final merge for
+        N > 1).  ``ev``: HIP events on the stream the launches are queued on,
+        bracketing the scan launch alone (``span="scan"``, the kernel the
+        headline's roofline prices) or every launch of the search, scan and
+        reduce (``span="search"``: the filter phases, thresholds, rescoring
+        and final select of the int8-image path)."""
 
-    def timed_leg():
+        def step(ev=None):
+            if ev is not None:
+                ev[0].record()
+            if qu8:  # fx_knn_search_ex: scan + merge in one call (the merge is ~1 % of it)
+                with eng.lock:
+                    eng.search_shard(sh, q, metric, k, None, od, orow)
+            else:
+                st = eng.scan(sh, q, metric, k)
+            if ev is not None and span == "scan":
+                ev[1].record()
+            if not qu8:
+                eng.reduce(sh, q, metric, k, st, od, orow)
+            if ev is not None and span == "search":
+                ev[1].record()
+            if use_dist:
+                if gloo:
+                    gd, gr = allgather_topk(od.cpu(), orow.cpu())
+                    gd, gr = gd.to(device), gr.to(device)
+                else:
+                    gd, gr = allgather_topk(od, orow)  # one RCCL all-gather over xGMI
+                md, mr = eng.merge(gd, gr, k)
+                return md, mr, gd, gr
+            return od.clone(), orow.clone(), None, None
+
+        return step
+
+    def timed_leg(step):
         """W untimed warmup steps, then exactly K steps bracketed by a barrier
         and a device synchronisation on both sides; (elapsed s max over ranks,
-        mean event-timed scan span ms max over ranks, last result)."""
+        mean event-timed span ms max over ranks, last result)."""
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
         for _ in range(args.warmup):
@@ -344,16 +386,17 @@ def main():
             elapsed, span = float(t[0]), float(t[1])
         return elapsed, span, res
 
-    def verify(res, what):
+    def verify(res, what, per_rank=None):
         """Sorted and complete; the planted rows first, in rank order; for
         N > 1 the merge equals the host's (distance, row) merge of the
-        gathered lists, bit for bit."""
+        gathered lists, bit for bit.  ``per_rank``: rows per rank when it is
+        not ``n`` (the strong-scaling leg's split of a fixed corpus)."""
         if args.no_verify:
             return
         rd, rr = res[0].cpu().numpy(), res[1].cpu().numpy()
         assert (rr >= 0).all() and np.all(np.diff(rd, axis=1) >= 0), f"{what}: result not sorted"
         if planted is not None and k >= world:
-            want = np.array([g * n + (g * 7919 + 12345) % n for g in range(world)])
+            want = np.array([planted_global(g, per_rank) for g in range(world)])
             assert (rr[0, :world] == want).all(), f"{what}: planted rows {rr[0, :world]} != {want}"
         if res[2] is not None:
             hd, hr = host_merge(res[2].cpu().numpy(), res[3].cpu().numpy(), k)
@@ -386,16 +429,46 @@ def main():
     # The headline: a single query runs the exact fused scan
     # over every row (option single_query_image=0); batches run the product
     # path (the bound filter over the filter image).
+    filt = not single and not qu8 and image is not None
     with _lib.options(single_query_image=0) if single else _nullctx():
-        elapsed, scan_ms, res = timed_leg()
+        elapsed, scan_ms, res = timed_leg(make_step(shard, "search" if filt else "scan"))
     verify(res, "headline")
+    head = res
+
+    # strong scaling (BASELINE's metric as worded: one 10M-row corpus at
+    # 1/2/4/8 GPUs): the same exact search over strong_rows rows in total,
+    # shard_rows(strong_rows, N, rank) per rank (a prefix of this rank's rows)
+    strong = None
+    if world > 1 and single and args.strong_rows > 0:
+        s_base, s_cnt = shard_rows(args.strong_rows, world, rank)
+        if s_cnt > n:
+            sys.exit(f"--strong-rows {args.strong_rows} needs {s_cnt} rows per rank (> --rows)")
+        s_shard = Shard(x[:s_cnt], s_base)
+        with _lib.options(single_query_image=0):
+            s_el, s_ms, s_res = timed_leg(make_step(s_shard, "scan"))
+        # planted rows beyond a rank's prefix are not in the strong corpus
+        if all((g * 7919 + 12345) % n < shard_rows(args.strong_rows, world, g)[1]
+               for g in range(world)):
+            verify(s_res, "strong", per_rank=args.strong_rows)
+        s_bytes = s_cnt * d * esize + nq * d * 4
+        strong = {
+            "scaling": "strong",
+            "total_rows": args.strong_rows,
+            "rows_per_gpu": s_cnt,
+            "ms_per_step": s_el * 1e3 / args.steps,
+            "value": args.strong_rows * nq * args.steps / s_el,
+            "unit": "vectors/s",
+            "kernel_ms": s_ms,
+            "frac": check_frac("strong.frac", s_bytes / (s_ms * 1e-3) / 1e9 / HBM_PEAK_GBS),
+            "what": "exact fused scan of each rank's 1/N of the corpus + RCCL all-gather + "
+                    "merge; ms_per_step includes the gather and merge, kernel_ms the scan only",
+        }
 
     # the product default for the same single query: the int8 filter image +
     # exact rescoring (bit-identical), timed as its own leg
     accel = None
     if single and image is not None:
-        head = res
-        a_el, a_ms, res = timed_leg()
+        a_el, a_ms, res = timed_leg(make_step(shard, "search"))
         verify(res, "accelerated")
         same = bool(np.array_equal(head[1].cpu().numpy(), res[1].cpu().numpy()) and np.array_equal(
             head[0].cpu().numpy().view(np.uint32), res[0].cpu().numpy().view(np.uint32)))
@@ -410,12 +483,14 @@ def main():
             "ms_per_step": a_el * 1e3 / args.steps,
             "vectors_per_s": n * world * nq * args.steps / a_el,
             "kernel_ms": a_ms,
-            "kernel": "fx::q64i::filter_img6_kernel (all phases) + thresholds + rescoring",
+            "kernel": "every launch of the search: query prep, fx::q64i::filter_img6_kernel "
+                      "(all phases), thresholds, rescoring, final select",
             "image_bytes": img_bytes,
             "image_build_ms": image_build_ms,
             "bytes_per_search": pass_bytes,
             "achieved_gbs_over_image": pass_bytes / (a_ms * 1e-3) / 1e9,
-            "frac_over_image": pass_bytes / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "frac_over_image": check_frac("accelerated_exact.frac_over_image",
+                                          pass_bytes / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS),
             "traffic": a_traffic,
             "traffic_over_image": (a_traffic / pass_bytes) if a_traffic else None,
             "bit_identical": same,
@@ -433,7 +508,6 @@ def main():
     scan_bytes = n * d * esize + nq * d * 4
     algo_bytes = scan_bytes
     tag = f"{n}x{d}_{args.dtype}_{args.metric}_k{k}_q{nq}"
-    filt = not single and not qu8 and image is not None
     if filt:
         # a batch streams the filter image and its row terms instead of the
         # rows (the rescoring reads a few thousand rows per query on top)
@@ -464,7 +538,33 @@ def main():
         roof["algorithmic_bytes"] = algo_bytes
         roof["mfma_tflops"] = 2.0 * n * nq * d / (scan_ms * 1e-3) / 1e12
         roof["mfma_peak_tflops"] = MFMA_F16_PEAK_TFS * (2 if bits == 8 else 1)
-    roof["frac"] = roof["achieved"] / roof["peak"]
+    roof["frac"] = check_frac("roofline.frac", roof["achieved"] / roof["peak"])
+    if "mfma_tflops" in roof:
+        check_frac("roofline.mfma", roof["mfma_tflops"] / roof["mfma_peak_tflops"])
+
+    # the single-process path a Flight server runs over every GPU of the node
+    # (engine._search_all): rank 0 alone, while the other ranks wait on the
+    # rendezvous store (no GPU kernel of theirs is spinning meanwhile)
+    serve = None
+    serve_devs = None
+    if args.serve_devices and not qu8:
+        serve_devs = [int(v) for v in args.serve_devices.split(",")]
+    elif world > 1 and single and not qu8 and torch.cuda.device_count() >= world:
+        serve_devs = list(range(world))
+    if serve_devs is not None and world > 1:
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            try:
+                serve = serve_leg(eng, serve_devs, n, d, k, metric, q, args,
+                                  head if world == len(serve_devs) else None)
+            except Exception as e:  # reported in the line; the rank-path legs stand
+                serve = {"error": f"{type(e).__name__}: {e}"}
+            finally:
+                store.set("fx_bench_serve_done", "1")
+        else:
+            store.wait(["fx_bench_serve_done"], datetime.timedelta(minutes=20))
+    elif serve_devs is not None:
+        serve = serve_leg(eng, serve_devs, n, d, k, metric, q, args, None)
 
     out = None
     if rank == 0:
@@ -505,14 +605,20 @@ def main():
                 **({"cluster": args.cluster} if args.cluster else {}),
                 **({"query": args.query} if args.query != "normal" else {}),
                 **({"options": args.opt} if args.opt else {}),
-                "parallelism": f"row-shard x{world}"
-                + ((" + gloo all-gather" if gloo else " + RCCL all-gather") if use_dist else ""),
+                "parallelism": f"row-shard x{world}, one process per GPU"
+                + ((" + gloo all-gather" if gloo else " + RCCL all-gather") if use_dist else "")
+                + (f"; strong leg: {args.strong_rows} rows over {world}" if strong else "")
+                + (f"; serve leg: one process over devices {serve_devs}, gathers "
+                   f"{'/'.join(serve.get('gathers', {}))}" if serve and "gathers" in serve
+                   else ""),
             },
             **({"filter_image": {"bits": bits, "bytes": img_bytes, "build_ms": image_build_ms,
                                  "note": "resident beside the corpus, built once per corpus "
                                          "version (not in ms_per_step)"}}
                if image is not None else {}),
             "roofline": roof,
+            **({"strong": strong} if strong is not None else {}),
+            **({"serve": serve} if serve is not None else {}),
             **({"accelerated_exact": accel} if accel is not None else {}),
             **({"configs2": batch} if batch is not None else {}),
             "cpu_baseline": cpu,
@@ -521,6 +627,81 @@ def main():
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()
+    return out
+
+
+def serve_leg(eng, devs, n, d, k, metric, q, args, rank_result):
+    """The Flight server's multi-GPU path (SURVEY §8(e), configs[3]/[4]'s
+    deployment): ONE process holding a row shard of n rows on each listed
+    device (the same rows and planted rows the one-process-per-GPU ranks
+    hold), searched by engine._search_all — every device's exact scan queued
+    back to back, then the per-device top-k exchanged over RCCL (one grouped
+    all-gather, the default for distinct devices) or peer copies, and merged on
+    the first device.  W + K searches per gather mode, timed from the host with
+    every device synchronised on both sides.  ``rank_result``: the
+    one-process-per-GPU legs' merged result, which each mode must equal bit
+    for bit."""
+    from fenix_amd import _lib, engine
+    from fenix_amd.engine import Engine, Shard
+
+    world = len(devs)
+    shards = []
+    for g, ordinal in enumerate(devs):
+        dv = torch.device("cuda", ordinal)
+        with torch.cuda.device(dv):
+            e = Engine.get(dv)
+            xs = torch.empty((n, d), dtype=torch.float32 if args.dtype == "f32" else torch.float16,
+                             device=dv)
+            e.fill(xs, seed=0, row_base=g * n, cluster=args.cluster)
+            if not args.no_verify:
+                plant_rows(xs, q.to(dv), args.metric, g, world)
+                torch.autograd.graph.increment_version(xs)
+            shards.append(Shard(xs, g * n))
+
+    def sync_all():
+        for o in sorted(set(devs)):
+            torch.cuda.synchronize(o)
+
+    # distinct devices: both exchanges; an ordinal repeated on one GPU (a
+    # rehearsal) merges its shards on that device with no exchange ("none")
+    ndev = len(set(devs))
+    modes = ["rccl", "p2p"] if ndev == len(devs) and ndev > 1 else ["p2p"] if ndev > 1 else ["none"]
+    out = {"devices": devs, "rows_per_device": n, "total_rows": n * world,
+           "what": "one process, exact scan per device shard, gather to the first device, "
+                   "fx_topk_merge (engine._search_all, the path Flight.search serves)",
+           "gathers": {}}
+    old = os.environ.get("FENIX_AMD_GATHER")
+    try:
+        for mode in modes:
+            os.environ["FENIX_AMD_GATHER"] = "p2p" if mode == "none" else mode
+            before = dict(engine.GATHERS)
+            with _lib.options(single_query_image=0):
+                for _ in range(args.warmup):
+                    engine._search_all(shards, q, metric, k)
+                sync_all()
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    rd, rr = engine._search_all(shards, q, metric, k)
+                sync_all()
+                el = time.perf_counter() - t0
+            used = {m: engine.GATHERS[m] - before[m] for m in before}
+            rec = {"ms_per_step": el * 1e3 / args.steps,
+                   "value": n * world * args.steps / el, "unit": "vectors/s",
+                   "gathers_used": used}
+            if mode != "none" and used.get(mode, 0) != args.warmup + args.steps:
+                raise RuntimeError(f"serve leg: asked for {mode}, ran {used}")
+            if rank_result is not None and not args.no_verify:
+                same = bool(np.array_equal(rr.cpu().numpy(), rank_result[1].cpu().numpy())
+                            and np.array_equal(rd.cpu().numpy().view(np.uint32),
+                                               rank_result[0].cpu().numpy().view(np.uint32)))
+                assert same, f"serve leg ({mode}) differs from the one-process-per-GPU result"
+                rec["equals_rank_path"] = same
+            out["gathers"][mode] = rec
+    finally:
+        if old is None:
+            os.environ.pop("FENIX_AMD_GATHER", None)
+        else:
+            os.environ["FENIX_AMD_GATHER"] = old
     return out
 
 
@@ -582,7 +763,8 @@ def batch_leg(eng, shard, image, img_bytes, n, d, k, args, nb=256, mname="cosine
         "kernel": "filter phases (int8 MFMA bound filter) + thresholds + rescoring + select",
         "bytes_per_search": pass_bytes,
         "achieved_gbs_over_image": pass_bytes / (span * 1e-3) / 1e9,
-        "frac_over_image": pass_bytes / (span * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "frac_over_image": check_frac("configs2.frac_over_image",
+                                      pass_bytes / (span * 1e-3) / 1e9 / HBM_PEAK_GBS),
         "mfma_tflops": 2.0 * n * nb * d / (span * 1e-3) / 1e12,
         "mfma_peak_tflops": MFMA_F16_PEAK_TFS * 2,
         "traffic": traffic,

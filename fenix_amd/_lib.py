@@ -44,6 +44,7 @@ SYMBOLS = (
     "fx_device_count",
     "fx_max_k",
     "fx_knn_workspace_bytes",
+    "fx_knn_workspace_bytes_img8",
     "fx_knn_search",
     "fx_knn_scan",
     "fx_knn_reduce",
@@ -140,6 +141,8 @@ def load() -> ctypes.CDLL:
         L.fx_max_k.restype = i64
         L.fx_knn_workspace_bytes.argtypes = [i64, i64, ci, i64, i64, ctypes.POINTER(sz)]
         L.fx_knn_workspace_bytes.restype = ci
+        L.fx_knn_workspace_bytes_img8.argtypes = [i64, i64, ci, i64, i64, ci, ctypes.POINTER(sz)]
+        L.fx_knn_workspace_bytes_img8.restype = ci
         L.fx_knn_search.argtypes = [vp, ci, i64, i64, i64, vp, i64, ci, i64, vp, vp, sz, vp, vp,
                                     vp]
         L.fx_knn_search.restype = ci
@@ -272,13 +275,23 @@ def _planned(key: tuple, compute):
     return hit
 
 
-def knn_workspace_bytes(n: int, d: int, dtype: int, nq: int, k: int) -> int:
+def knn_workspace_bytes(n: int, d: int, dtype: int, nq: int, k: int, img8: bool = True) -> int:
+    """fx_knn_workspace_bytes_img8: workspace of a search of this shape that is
+    (img8) or is not given an int8 filter image (4x the candidate buffers), on
+    the current device (its CU count sizes the scan's lists: part of the key)."""
     def compute() -> int:
         out = ctypes.c_size_t(0)
-        check(load().fx_knn_workspace_bytes(n, d, dtype, nq, k, ctypes.byref(out)))
+        check(load().fx_knn_workspace_bytes_img8(n, d, dtype, nq, k, int(bool(img8)),
+                                                 ctypes.byref(out)))
         return int(out.value)
 
-    return _planned(("ws", n, d, dtype, nq, k), compute)
+    return _planned(("ws", _current_device(), n, d, dtype, nq, k, bool(img8)), compute)
+
+
+def _current_device() -> int:
+    import torch
+
+    return torch.cuda.current_device() if torch.cuda.is_available() else -1
 
 
 def filter_image_used(n: int, d: int, dtype: int, nq: int, k: int, metric: int) -> bool:

@@ -814,6 +814,11 @@ int fx_set_option(const char* name, int64_t value) {
     set_error("unknown option %s", name ? name : "(null)");
     return FX_EINVAL;
   }
+  if (i == kOptI8MaxK && (value < 0 || value > kSelectMaxK)) {
+    set_error("option i8_max_k=%lld outside [0, %d] (the select kernel's LDS bound)",
+              (long long)value, kSelectMaxK);
+    return FX_EINVAL;
+  }
   g_opts[i].store(value, std::memory_order_relaxed);
   return FX_OK;
 }
@@ -846,6 +851,11 @@ int64_t fx_max_k(void) { return kMaxK; }
 
 int fx_knn_workspace_bytes(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k,
                            size_t* out_bytes) {
+  return fx_knn_workspace_bytes_img8(n, d, dtype, nq, k, 1, out_bytes);
+}
+
+int fx_knn_workspace_bytes_img8(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k,
+                                int img8, size_t* out_bytes) {
   if (!out_bytes) {
     set_error("out_bytes is null");
     return FX_EINVAL;
@@ -859,9 +869,11 @@ int fx_knn_workspace_bytes(int64_t n, int64_t d, int dtype, int64_t nq, int64_t 
   size_t best = 0;
   for (int metric = 0; metric < 3; ++metric) {
     for (int aligned = 0; aligned < 2; ++aligned) {
-      for (int img8 = 0; img8 < 2; ++img8) {
+      // with an int8 image a search may still plan without it (k above
+      // i8_max_k): the larger of both; without one, the image-free plan only
+      for (int with8 = 0; with8 < (img8 ? 2 : 1); ++with8) {
         SearchLayout s;
-        rc = plan_search(n, d, dtype, nq, k, metric, aligned != 0, &s, img8 != 0);
+        rc = plan_search(n, d, dtype, nq, k, metric, aligned != 0, &s, with8 != 0);
         if (rc) return rc;
         if (s.total > best) best = s.total;
       }

@@ -11,6 +11,10 @@ constexpr int kModeDist = 1;
 // Per-query append counters of the batched kernels sit 128 B apart: every
 // counter in its own cache line, so the L2 channels serialise fewer atomics.
 constexpr int kCountStride = 32;
+// largest k of the one-workgroup select_kernel (knn_batch.hip): its LDS holds a
+// 16 384-entry chunk plus the k kept so far rounded up to a power of two, which
+// fits the 160 KB of a CU up to 2 048; also the bound of option "i8_max_k"
+constexpr int kSelectMaxK = 2048;
 
 // Process-wide options (fx_set_option, include/fenix_knn.h); relaxed atomics.
 enum Option : int {

@@ -772,7 +772,7 @@ int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t r
                            const float* Q, const float* qnorm, int64_t nq, const uint64_t* keys,
                            int64_t cap, uint32_t* count, bool zero_count, int k, int metric,
                            uint64_t* thr, hipStream_t stream) {
-  if (k > kSelectEntries / 2 || k > cap) {
+  if (k > kSelectMaxK || k > cap) {
     set_error("exact threshold: k %d beyond cap %lld", k, (long long)cap);
     return FX_EUNSUPPORTED;
   }
@@ -787,7 +787,7 @@ int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t r
 
 int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint32_t* count,
                             bool zero_count, int k, uint64_t* thr, hipStream_t stream) {
-  if (k > kSelectEntries / 2) {
+  if (k > kSelectMaxK) {
     set_error("sample threshold: k %d too large", k);
     return FX_EUNSUPPORTED;
   }
@@ -799,7 +799,7 @@ int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint3
 int launch_final_select(const uint64_t* keys, int64_t nq, int64_t cap, const uint32_t* count,
                         int k, float* out_dist, int64_t* out_row, const uint64_t* alt,
                         int64_t alt_m, int64_t alt_gate, hipStream_t stream) {
-  if (k > kSelectEntries / 2) {
+  if (k > kSelectMaxK) {
     set_error("final select: k %d too large", k);
     return FX_EUNSUPPORTED;
   }

@@ -82,12 +82,17 @@ def _chunk_values(chunk: pa.FixedSizeListArray, np_dtype: np.dtype) -> np.ndarra
     Like the reference's ``io.torch.from_arrow`` (src/fenix/io/torch/torch.py:6-10)
     validity is ignored (a null slot's stored values are scanned), but unlike it
     the parent's array offset is honoured (from_arrow reads ``.values`` from
-    element 0 even for a sliced array).
+    element 0 even for a sliced array).  Nulls inside the VALUES (a null slot
+    built from a Python ``None``) raise what the reference's ``from_dlpack``
+    raises there, ``ArrowTypeError`` (tests/golden g7_nulls); a null slot whose
+    values are stored (validity on the list array only) is scanned.
     """
     if isinstance(chunk, pa.ExtensionArray):
         chunk = chunk.storage
     d = chunk.type.list_size
     vals = chunk.values
+    if vals.null_count and vals.slice(chunk.offset * d, len(chunk) * d).null_count:
+        raise pa.ArrowTypeError("Can only use DLPack on arrays with no nulls.")
     buf = vals.buffers()[1]
     start = (vals.offset + chunk.offset * d) * np_dtype.itemsize
     count = len(chunk) * d
@@ -538,9 +543,9 @@ class Engine:
         if shard.dtype_id == _lib.DTYPE_QU8:
             self._search_ex(shard, None, -1, queries, metric, k, mask, out_dist, out_row)
             return
-        nbytes = _lib.knn_workspace_bytes(shard.n, shard.d, shard.dtype_id, nq, k)
-        ws = self._workspace(nbytes)
         img, info, bits = self.filter_image(shard, nq, k, metric)
+        ws = self._workspace(_lib.knn_workspace_bytes(shard.n, shard.d, shard.dtype_id, nq, k,
+                                                      img8=bits == 8))
         self._hold(shard.data)
         L = _lib.load()
         _lib.check(
@@ -581,9 +586,9 @@ class Engine:
         pair never plans differently (an image evicted or rebuilt in between
         would make fx_knn_reduce read a filter workspace as scan lists)."""
         nq = queries.shape[0]
-        nbytes = _lib.knn_workspace_bytes(shard.n, shard.d, shard.dtype_id, nq, k)
-        ws = self._workspace(nbytes)
         img, info, bits = self.filter_image(shard, nq, k, metric)
+        ws = self._workspace(_lib.knn_workspace_bytes(shard.n, shard.d, shard.dtype_id, nq, k,
+                                                      img8=bits == 8))
         self._hold(shard.data)
         L = _lib.load()
         _lib.check(
@@ -867,6 +872,25 @@ def search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: i
     return _search_all(shards, queries, metric, k, masks, counts)
 
 
+# how many multi-device searches gathered their lists each way (bench.py, tests)
+GATHERS: Dict[str, int] = {"rccl": 0, "p2p": 0}
+
+
+def gather_mode(devs: Sequence[torch.device]) -> str:
+    """How ``_search_all`` gathers per-device top-k lists: ``rccl`` (one
+    grouped RCCL all-gather over xGMI, fx_allgather_topk: SURVEY §8(e)'s
+    exchange, the default for distinct devices) or ``p2p`` (a peer copy per
+    device to the first one; the only choice when an ordinal repeats, since
+    RCCL takes one rank per device).  ``FENIX_AMD_GATHER`` overrides."""
+    env = os.environ.get("FENIX_AMD_GATHER", "").strip()
+    distinct = len({d.index for d in devs}) == len(devs)
+    if env == "p2p" or not distinct:
+        return "p2p"
+    if env in ("", "rccl"):
+        return "rccl"
+    raise ValueError(f"FENIX_AMD_GATHER={env!r}: expected rccl or p2p")
+
+
 def _search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: int,
                 masks: Optional[Sequence[Optional[torch.Tensor]]] = None,
                 counts: Optional[Sequence[Optional[int]]] = None,
@@ -876,11 +900,11 @@ def _search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: 
     Each device's shards are searched by that device's Engine.  No library
     call waits for the host (the batched path's overflow fallback is gated on
     the device, fx_knn_reduce), so this loop queues every device's scan and
-    merge back to back and the devices scan concurrently; the per-device
-    [nq, k] results are copied to the first device (peer-to-peer over xGMI, a
-    few KB) and merged there by fx_topk_merge.  Single process: the gather is
-    a copy, not a collective (the one-process-per-GPU path uses RCCL,
-    distributed.py).
+    merge back to back and the devices scan concurrently.  The per-device
+    [nq, k] results are then exchanged as ``gather_mode`` says: one RCCL
+    all-gather over xGMI (distinct devices) or peer copies to the first
+    device, and merged there by fx_topk_merge.  (The one-process-per-GPU
+    path uses torch.distributed's RCCL all-gather, distributed.py.)
     """
     groups: Dict[torch.device, List[int]] = {}
     for i, s in enumerate(shards):
@@ -895,8 +919,10 @@ def _search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: 
     if len(per) == 1:
         return per[0]
     devs = list(groups)
-    if os.environ.get("FENIX_AMD_GATHER", "p2p") == "rccl":
+    if gather_mode(devs) == "rccl":
+        GATHERS["rccl"] += 1
         return DeviceComm.get(devs).gather_merge(per, k)
+    GATHERS["p2p"] += 1
     dev0 = next(iter(groups))
     with torch.cuda.device(dev0):
         eng0 = Engine.get(dev0)
@@ -910,9 +936,8 @@ class DeviceComm:
     """fx_comm_init_all over distinct devices (one RCCL rank each), cached.
 
     ``gather_merge`` all-gathers every device's [nq, k] top-k with one grouped
-    fx_allgather_topk and merges on the first device.  ``search_all`` uses it
-    when FENIX_AMD_GATHER=rccl; the default gathers with peer copies (the lists
-    are a few KB, a copy per device is one xGMI hop)."""
+    fx_allgather_topk and merges on the first device.  ``_search_all`` uses
+    it for distinct devices unless FENIX_AMD_GATHER=p2p (``gather_mode``)."""
 
     _cache: Dict[tuple, "DeviceComm"] = {}
     _clock = threading.Lock()

@@ -17,6 +17,7 @@ from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
 import pyarrow as pa
+import pyarrow.compute as pc
 import torch
 
 from .. import engine as _engine
@@ -24,7 +25,8 @@ from . import arrow, table
 
 _lock = threading.Lock()
 _TABLES: Dict[str, Tuple[tuple, pa.Table]] = {}  # path -> (stat key, mmap'd table)
-_COMBINED: Dict[tuple, pa.Array] = {}  # (version, column) -> single-chunk column
+# (version, column) -> single-chunk column; (version, column, "null") -> null slots
+_COMBINED: Dict[tuple, object] = {}
 _CODES: Dict[tuple, torch.Tensor] = {}  # (stat key, column, device) -> int64 [rows]
 
 
@@ -66,6 +68,18 @@ def combined(version: tuple, name: str, col: pa.ChunkedArray) -> pa.Array:
         with _lock:
             _COMBINED[key] = comb
     return comb
+
+
+def null_mask(version: tuple, name: str, col: pa.ChunkedArray) -> np.ndarray:
+    """bool[rows]: the null slots of a column (cached per file version)."""
+    key = (version, name, "null")
+    with _lock:
+        hit = _COMBINED.get(key)
+    if hit is None:
+        hit = pc.is_null(col).to_numpy(zero_copy_only=False).astype(bool)
+        with _lock:
+            _COMBINED[key] = hit
+    return hit
 
 
 def shards(parts, column: str, devs) -> List[Tuple[_engine.Shard, int, int]]:

@@ -142,22 +142,69 @@ def take_rows(data: pa.Table, rows: np.ndarray) -> pa.Table:
     return pa.Table.from_arrays(cols, schema=data.schema)
 
 
-def _gather_vectors(shards, rows: np.ndarray, type: pa.DataType) -> pa.Array:
+def _gather_vectors(shards, rows: np.ndarray, type: pa.DataType,
+                    null: np.ndarray | None = None) -> pa.Array:
     """The k winning embeddings, read back from their HBM shards (they are the
     stored Arrow values, staged verbatim) instead of gathered from Arrow
-    chunks: a few KB over PCIe instead of k chunk lookups."""
+    chunks (index.py:166's take): one H2D of (result position, local row)
+    pairs per device, an ``index_select`` per shard placed by ``index_copy_``
+    into one result buffer on the first shard's device (other devices' rows
+    travel there peer to peer), and ONE D2H into pinned memory with one
+    synchronisation — not a round trip per shard (configs[4]'s 8 shards:
+    0.63 ms -> see profiles/r05_cfg4_serving_profile.md).  ``null``: which
+    result rows are null slots of the column; their stored values are
+    gathered like any other (they were scanned) and the slot stays null, as
+    index.py:166's ``take`` keeps validity (tests/golden g7_nulls)."""
     d = _engine.list_size(type)
     _, tdt, ndt = _engine.value_dtype(type)
-    out = np.empty((rows.size, d), dtype=ndt)
-    for s in shards:
-        sel = np.nonzero((rows >= s.row_base) & (rows < s.row_base + s.n))[0]
-        if sel.size:
-            idx = torch.from_numpy(rows[sel] - s.row_base).to(s.data.device)
-            out[sel] = s.data.index_select(0, idx).cpu().numpy()
+    m = rows.size
+    if m == 0 or not shards:
+        out = np.empty((m, d), dtype=ndt)
+    else:
+        bases = np.array([s.row_base for s in shards], dtype=np.int64)
+        which = np.searchsorted(bases, rows, side="right") - 1  # shards are in row order
+        dev0 = shards[0].data.device
+        with torch.cuda.device(dev0):
+            acc = torch.empty((m, d), dtype=shards[0].data.dtype, device=dev0)
+            by_dev = {}
+            for i, s in enumerate(shards):
+                by_dev.setdefault(s.data.device, []).append(i)
+            for dev, idx in by_dev.items():
+                # (position in the result, local row) of every row this device holds
+                pos = [np.nonzero(which == i)[0] for i in idx]
+                sizes = [p.size for p in pos]
+                if not sum(sizes):
+                    continue
+                pairs = np.empty((2, sum(sizes)), dtype=np.int64)
+                pairs[0] = np.concatenate(pos)
+                pairs[1] = rows[pairs[0]] - np.repeat(bases[idx], sizes)
+                with torch.cuda.device(dev):
+                    pd = torch.from_numpy(pairs).to(dev)
+                    off = 0
+                    for i, c in zip(idx, sizes):
+                        if c:
+                            g = shards[i].data.index_select(0, pd[1, off : off + c])
+                            p = pd[0, off : off + c]
+                            if dev != dev0:
+                                g, p = g.to(dev0), p.to(dev0)
+                            acc.index_copy_(0, p, g)
+                        off += c
+                    if dev != dev0:  # the peer copies above read on this device's stream
+                        torch.cuda.current_stream(dev0).wait_stream(torch.cuda.current_stream(dev))
+            host = torch.empty((m, d), dtype=acc.dtype, pin_memory=True)
+            host.copy_(acc, non_blocking=True)
+            torch.cuda.current_stream(dev0).synchronize()
+        out = host.numpy().view(ndt)
+    mask = pa.array(null) if null is not None and null.any() else None
+    lists = pa.FixedSizeListArray.from_arrays(pa.array(out.ravel()), list_size=d, mask=mask)
     if isinstance(type, pa.ExtensionType):  # quint8 codes: same type, same parameters
-        storage = pa.FixedSizeListArray.from_arrays(pa.array(out.ravel()), list_size=d)
-        return pa.ExtensionArray.from_storage(type, storage.cast(type.storage_type))
-    return pa.FixedSizeListArray.from_arrays(pa.array(out.ravel()), list_size=d).cast(type)
+        return pa.ExtensionArray.from_storage(type, lists.cast(type.storage_type))
+    return lists.cast(type)
+
+
+def _null_mask(col: pa.ChunkedArray) -> np.ndarray:
+    """bool[rows]: which slots of ``col`` are null."""
+    return pc.is_null(col).to_numpy(zero_copy_only=False).astype(bool)
 
 
 def _take_columns(data: pa.Table, cols: List[str], rows: np.ndarray, column: str, shards,
@@ -167,8 +214,12 @@ def _take_columns(data: pa.Table, cols: List[str], rows: np.ndarray, column: str
     arrays = []
     for c in cols:
         col = data.column(c)
-        if c == column and col.null_count == 0:
-            arrays.append(_gather_vectors(shards, rows, col.type))
+        if c == column:
+            null = None
+            if col.null_count:
+                null = (_resident.null_mask(version, c, col) if version is not None
+                        else _null_mask(col))[rows]
+            arrays.append(_gather_vectors(shards, rows, col.type, null))
         elif version is None:
             arrays.append(_take_chunked(col, rows))
         else:

@@ -88,7 +88,8 @@ int fx_device_count(int* out);
  *   "single_query_image"  1  0: single queries keep the exact scan even when
  *                            an int8 filter image is supplied
  *   "i8_max_k"          256  largest k an int8 filter image serves (larger k:
- *                            the fp16 image / f32 rows, or the exact scan)
+ *                            the fp16 image / f32 rows, or the exact scan);
+ *                            at most 2048 (FX_EINVAL above)
  *   "img6"                1  1: int8-image batches of <= 128 queries (single
  *                            queries included) run the resident-query-slice
  *                            kernel; 2: larger batches too (as several
@@ -128,6 +129,14 @@ int64_t fx_max_k(void);
  */
 int fx_knn_workspace_bytes(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k,
                            size_t* out_bytes);
+/*
+ * The same for a search that is (img8 = 1) or is not (img8 = 0) given an int8
+ * filter image (fx_knn_scan_img8 / fx_knn_search_img8 with a non-null image).
+ * An int8-image plan holds 4x the candidate buffers of the image-free one;
+ * fx_knn_workspace_bytes is the img8 = 1 answer, enough for either.
+ */
+int fx_knn_workspace_bytes_img8(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k,
+                                int img8, size_t* out_bytes);
 
 /*
  * Exact k-nearest-neighbour search of nq queries over one row-major corpus

@@ -2,7 +2,7 @@
 
 Run ONLY in the build container, where the reference checkout exists:
 
-    python tests/golden/make_golden.py [--only-g6]
+    python tests/golden/make_golden.py [--only-g6 | --only-g7]
 
 It imports fenix from /root/reference/src (Python 3.10 needs the
 ``typing.Self`` shim: fenix/flight.py:5 imports it, fenix wants >= 3.11),
@@ -127,18 +127,95 @@ def g6_fp16(fenix, root) -> dict:
     return meta
 
 
+G7_NULLS = [0, 3, 17, 999, 1000, 1777, 2499]
+
+
+def g7_corpus():
+    """G7's corpus: fill_normal rows, row 17 = query 0 and row 1777 = query 1
+    + 0.01 (so null rows rank first), and the null slots G7_NULLS."""
+    n, d = 2500, 64
+    x = fill_normal(n, d, seed=15)
+    q = fill_normal(3, d, seed=16)
+    x[17] = q[0]
+    x[1777] = q[1] + np.float32(0.01)
+    return x, q
+
+
+def g7_nulls(fenix, root) -> dict:
+    """G7: null embedding slots (index.py:161-170 + io/torch/torch.py:6-10).
+
+    (a) the parent list array carries the validity bitmap and the child
+    values stay intact (FixedSizeListArray.from_arrays(values, mask=...)):
+    the reference scans a null slot's stored values like any other row
+    (from_dlpack of the child ignores the parent's validity), ranks it, and
+    the result's vector column is null there (Table.take keeps validity).
+    Recorded for maxval 10 (select path), None and 5000 > rows (whole table
+    in row order), with each result row's vector validity.
+    (b) nulls in the child values (a null slot built from Python None): the
+    UDF's from_dlpack raises; the error type and message are recorded."""
+    x, q = g7_corpus()
+    n, d = x.shape
+    mask = np.zeros(n, dtype=bool)
+    mask[G7_NULLS] = True
+    vt = pa.list_(pa.float32(), d)
+    schema = pa.schema({"id": pa.int64(), "vector": vt})
+    batches = []
+    for s in range(0, n, 1000):
+        e = min(n, s + 1000)
+        arr = pa.FixedSizeListArray.from_arrays(pa.array(x[s:e].ravel()), list_size=d,
+                                                mask=pa.array(mask[s:e]))
+        batches.append(pa.record_batch([pa.array(np.arange(s, e, dtype=np.int64)), arr],
+                                       names=["id", "vector"]))
+    fenix.io.table.make(root, "g7_nulls", pa.RecordBatchReader.from_batches(schema, batches))
+    rec = {}
+    metrics = ["l2", "cosine", "inner_product"]
+    for metric in metrics:
+        for mv in (10, None, 5000):
+            tag = f"{metric}_{'all' if mv is None else mv}"
+            rows = n if mv is None or mv >= n else mv
+            ids = np.empty((len(q), rows), dtype=np.int64)
+            dist = np.empty((len(q), rows), dtype=np.float32)
+            null = np.empty((len(q), rows), dtype=bool)
+            for i, qv in enumerate(q):
+                t = fenix.io.index.call(root, None, "g7_nulls", "vector", target=qv,
+                                        metric=metric, maxval=mv)
+                ids[i] = t.column("id").to_numpy()
+                dist[i] = t.column("__DISTANCE__").to_numpy()
+                null[i] = t.column("vector").is_null().to_numpy(zero_copy_only=False)
+                rec["schema"] = str(t.schema)
+            rec[f"{tag}_ids"], rec[f"{tag}_dist"], rec[f"{tag}_null"] = ids, dist, null
+    # (b) child-level nulls
+    rows_py = [None if m else [float(v) for v in r] for r, m in zip(x[:1000], mask[:1000])]
+    arr = pa.array(rows_py, type=vt)
+    b = pa.record_batch([pa.array(np.arange(1000, dtype=np.int64)), arr], names=["id", "vector"])
+    fenix.io.table.make(root, "g7_child_nulls", pa.RecordBatchReader.from_batches(schema, [b]))
+    try:
+        fenix.io.index.call(root, None, "g7_child_nulls", "vector", target=q[0], metric="l2",
+                            maxval=10)
+        child_error = ""
+    except Exception as e:  # recorded, not raised: this is the expected outcome
+        child_error = f"{type(e).__name__}: {e}"
+    meta = dict(kind="direct_nulls", n=n, d=d, seed=15, qseed=16, nq=3, chunk=1000, cluster=0,
+                nulls=G7_NULLS, planted={"17": "q0", "1777": "q1 + 0.01"}, sha256=_sha(x),
+                metrics=metrics, maxvals=[10, None, 5000], child_nulls_error=child_error)
+    np.savez_compressed(os.path.join(HERE, "g7_nulls.npz"), meta=json.dumps(meta), **rec)
+    return meta
+
+
 def main() -> None:
     fenix = _import_fenix()
     root = tempfile.mkdtemp(prefix="fenix_golden_")
     manifest = {}
-    if "--only-g6" in sys.argv:  # add the fp16 case to an existing manifest
-        with open(os.path.join(HERE, "MANIFEST.json")) as f:
-            manifest = json.load(f)
-        manifest["g6_fp16"] = g6_fp16(fenix, root)
-        with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
-            json.dump(manifest, f, indent=1, sort_keys=True)
-        print("wrote g6_fp16")
-        return
+    only = {"--only-g6": ("g6_fp16", g6_fp16), "--only-g7": ("g7_nulls", g7_nulls)}
+    for flag, (name, fn) in only.items():
+        if flag in sys.argv:  # add one case to an existing manifest
+            with open(os.path.join(HERE, "MANIFEST.json")) as f:
+                manifest = json.load(f)
+            manifest[name] = fn(fenix, root)
+            with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
+                json.dump(manifest, f, indent=1, sort_keys=True)
+            print("wrote", name)
+            return
 
     # G1: generic N(0,1)-like corpora, ragged last chunk (8192 = 8*1000 + 192)
     for d in (128, 768):
@@ -206,6 +283,7 @@ def main() -> None:
     manifest["g4_flight"] = meta
 
     manifest["g6_fp16"] = g6_fp16(fenix, root)
+    manifest["g7_nulls"] = g7_nulls(fenix, root)
 
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)

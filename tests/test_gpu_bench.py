@@ -67,21 +67,42 @@ def test_bench_rccl_path_one_rank():
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout
     rec = json.loads(lines[0])
-    assert rec["config"]["parallelism"] == "row-shard x1 + RCCL all-gather"
+    assert rec["config"]["parallelism"] == "row-shard x1, one process per GPU + RCCL all-gather"
     assert rec["n_gpus"] == 1 and rec["value"] > 0
 
 
 def test_bench_gpus_n_launches_n_ranks():
     """`bench.py --gpus 2` without a launcher starts 2 ranks itself (here
     with gloo, two ranks sharing the one GPU of the box: RCCL refuses a
-    duplicate device) and reports n_gpus 2 over 2 x rows."""
+    duplicate device) and reports n_gpus 2 over 2 x rows, the strong-scaling
+    leg (--rows in total, half per rank) and the single-process serve leg
+    (rank 0 alone, two shards through engine._search_all, merged on the one
+    device since the ordinal repeats), whose result bench.py checks against
+    the ranks' merge."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     rec = run_bench("--gpus", "2", "--dist-backend", "gloo", "--rows", "200000", "--steps", "3",
-                    "--warmup", "1", "--no-cpu-baseline", env=env)
+                    "--warmup", "1", "--no-cpu-baseline", "--serve-devices", "0,0", env=env)
     assert rec["n_gpus"] == 2
     assert rec["config"]["total_rows"] == 400000
-    assert rec["config"]["parallelism"] == "row-shard x2 + gloo all-gather"
+    assert rec["config"]["parallelism"].startswith(
+        "row-shard x2, one process per GPU + gloo all-gather; strong leg: 200000 rows over 2")
+    strong = rec["strong"]
+    assert strong["total_rows"] == 200000 and strong["rows_per_gpu"] == 100000
+    assert 0 < strong["frac"] <= 1
+    serve = rec["serve"]
+    assert "error" not in serve, serve
+    assert list(serve["gathers"]) == ["none"]
+    assert serve["gathers"]["none"]["equals_rank_path"] is True
+
+
+def test_bench_serve_devices_one_rank():
+    """--serve-devices on a single rank (no process group): one process, three
+    row shards on the one GPU, merged there."""
+    rec = run_bench("--rows", "200000", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                    "--no-accelerated", "--serve-devices", "0,0,0")
+    serve = rec["serve"]
+    assert serve["total_rows"] == 600000 and serve["gathers"]["none"]["value"] > 0
 
 
 def test_bench_gpus_must_match_world_size():

@@ -96,6 +96,29 @@ def test_code_assign_float16_and_tail_rows(eng, metric):
     _assign_ok(x.astype(np.float32), cw, metric, idx.cpu().numpy())
 
 
+@pytest.mark.parametrize("metric", METRICS)
+def test_code_assign_repeats_bit_exactly(eng, metric):
+    """The MFMA code assignment repeated on the same rows returns the same
+    indices and the same distance bits every time: an accumulator read before
+    its MFMA landed (the hazard DESIGN.md §3.6e audits) would move a near-tie
+    index or a distance's low bits between runs.  Many rows (every CU busy,
+    two waves per SIMD), wide codebooks, a tail tile."""
+    n, d, nb, ks = 200_003, 256, 2, 256
+    x = torch.empty((n, d), dtype=torch.float32, device=eng.device)
+    eng.fill(x, seed=47, cluster=1000)
+    cw = torch.from_numpy(O.fill_normal(nb * ks, d, seed=48).reshape(nb, ks, d))
+    ref = None
+    for _ in range(6):
+        idx, _, dist = eng.code_assign(x, cw, _lib.METRICS[metric], index=True, code=False,
+                                       dist=True)
+        got = (idx.cpu().numpy(), dist.cpu().numpy().view(np.uint32))
+        if ref is None:
+            ref = got
+            continue
+        np.testing.assert_array_equal(got[0], ref[0], err_msg="indices moved")
+        np.testing.assert_array_equal(got[1], ref[1], err_msg="distance bits moved")
+
+
 def test_code_assign_unaligned_rows(eng):
     n, d, nb, ks = 700, 33, 2, 8  # odd d: scalar staging path
     x = O.fill_normal(n, d, seed=45)

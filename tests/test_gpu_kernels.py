@@ -873,20 +873,23 @@ def test_small_batches_rescore_all_and_fallback_lists(eng, metric):
     eng.clear_images()
 
 
-@pytest.mark.parametrize("img6", [0, 2])
+@pytest.mark.parametrize("img6", [0, 1, 2])
 def test_filter_candidate_counts_repeat_exactly(eng, img6):
     """The same int8-image search repeated appends exactly the same
     candidates: a kernel that reads a product, a query chunk or a row term
     before it has landed shows up as counts moving between identical runs
     long before it moves a result (tools/race_check.py; the resident-slice
     kernel without its pre-epilogue barrier moved in 201 of 232 repetitions,
-    DESIGN.md 3.6d item 7)."""
+    DESIGN.md 3.6d item 7).  nq 1-64 run the q64i build (img6 1 and 2: its
+    resident-slice kernel, configs[1]'s product default for a single query),
+    65 the q128 build, 256 the 256-query tiles or two slices;
+    batch_min_queries=1 sends the single query through the filter."""
     n, d, k = 70_000, 768, 30
     x = torch.from_numpy(_extreme_rows(n, d, 49)).to(eng.device)
     eng.clear_images()
-    for nq in (65, 256):
+    for nq in (1, 2, 16, 64, 65, 256):
         q = torch.from_numpy(O.fill_normal(nq, d, seed=60 + nq)).to(eng.device)
-        with _lib.options(img6=img6, filter_image=8):
+        with _lib.options(img6=img6, filter_image=8, batch_min_queries=1):
             ref = None
             for _ in range(8):
                 st = eng.scan(Shard(x, 0), q, _lib.METRICS["l2"], k)

@@ -5,13 +5,23 @@ then Flight.search (flight.py:242-288) -> Server.do_exchange (flight.py:62-77)
 eight row shards on the one GPU, exactly the 8-GPU deployment's split and
 merge) -> inner product, k = 1 000 -> the ~3 MB reply with every column.
 Row ids are checked against the float64 oracle, the gathered vectors against
-the source rows, the halffloat distances at fp16 resolution."""
+the source rows, the halffloat distances at fp16 resolution.
+
+The latency is timed the way a client sees it: a torch-free client process
+(tools/bench_flight.py --client) over loopback gRPC, 20 warm searches, with a
+bound on the median.  The checks above run in this process, which also hosts
+the server; a search timed from here measured 28-29 ms in round 4 against
+5.3 ms from a separate client (profiles/r05_cfg4_serving_profile.md): the
+in-process client shares the server's interpreter and GIL, and this process
+imports torch, which a client never does."""
 
 from __future__ import annotations
 
 import json
 import os
 import socket
+import subprocess
+import sys
 import time
 
 import numpy as np
@@ -25,6 +35,10 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 SHARDS, PER_SHARD, D, K = 8, 500_000, 1536, 1000
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# median of 20 warm searches from a separate client process (measured 5.3 ms
+# before the one-sync vector gather, profiles/r05_cfg4_serving_profile.md)
+MEDIAN_MS_BOUND = 6.0
 VECTOR = pa.list_(pa.float16(), D)
 SCHEMA = pa.schema({"id": pa.int64(), "vector": VECTOR})
 
@@ -94,6 +108,15 @@ def test_configs4_flight_8_shards_f16_ip_k1000(tmp_path, monkeypatch):
             assert np.all(np.abs(got - od[0]) <= 2.0 ** -10 * np.abs(od[0]) + 2.0 ** -14)
             vec = np.stack(r.column("vector").to_numpy(zero_copy_only=False))
             np.testing.assert_array_equal(vec.view(np.uint16), x16[ids].view(np.uint16))
+        # the latency a client sees: a torch-free client process, warm searches
+        cmd = [sys.executable, os.path.join(ROOT, "tools", "bench_flight.py"), "--client",
+               "--port", str(port), "--d", str(D), "--k", str(K), "--metric", "inner_product",
+               "--dtype", "f16", "--reps", "20", "--source", "cfg4/source"]
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=ROOT)
+        assert out.returncode == 0, out.stderr[-2000:]
+        client = json.loads(out.stdout.strip().splitlines()[-1])
+        assert client["torch_imported"] is False
+        median_ms = float(np.median(client["lat_ms"]))
         # the column was staged as 8 row shards (one per listed device)
         (entry,) = [e for e in engine.CACHE._entries.values() if "cfg4" in e.key[0]]
         assert len(entry.pieces) == SHARDS
@@ -101,7 +124,10 @@ def test_configs4_flight_8_shards_f16_ip_k1000(tmp_path, monkeypatch):
         os.makedirs("gpurun_out", exist_ok=True)
         with open(os.path.join("gpurun_out", "cfg4_serving_test.json"), "w") as f:
             json.dump({"rows": n, "d": D, "k": K, "shards": SHARDS,
-                       "flight_search_s": times, "near_ties": near_ties}, f)
+                       "client_process_lat_ms": client["lat_ms"],
+                       "client_process_median_ms": median_ms,
+                       "inprocess_flight_search_s": times, "near_ties": near_ties}, f)
+        assert median_ms <= MEDIAN_MS_BOUND, (median_ms, client["lat_ms"])
     finally:
         server.shutdown()
         engine.CACHE.clear()

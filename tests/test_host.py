@@ -84,6 +84,28 @@ def test_chunk_values_honours_offsets():
     np.testing.assert_array_equal(t.numpy(), x.reshape(10, 4)[3:7])
 
 
+def test_chunk_values_null_slots():
+    """A null slot with stored values is staged like any row (the reference's
+    from_dlpack ignores the list's validity); nulls inside the values raise
+    the reference's ArrowTypeError (tests/golden g7_nulls), from staging and
+    from io.torch.from_arrow alike."""
+    x = np.arange(40, dtype=np.float32)
+    mask = pa.array([False, True] + [False] * 8)
+    arr = pa.FixedSizeListArray.from_arrays(pa.array(x), list_size=4, mask=mask)
+    assert arr.null_count == 1
+    np.testing.assert_array_equal(engine._chunk_values(arr, np.dtype(np.float32)),
+                                  x.reshape(10, 4))
+    child = pa.array([[1.0, 2.0], None, [3.0, 4.0]], type=pa.list_(pa.float32(), 2))
+    assert child.values.null_count == 2
+    with pytest.raises(pa.ArrowTypeError, match="DLPack on arrays with no nulls"):
+        engine._chunk_values(child, np.dtype(np.float32))
+    with pytest.raises(pa.ArrowTypeError, match="DLPack on arrays with no nulls"):
+        io_torch.from_arrow(child)
+    # a slice that excludes the null-valued slot stages
+    np.testing.assert_array_equal(engine._chunk_values(child.slice(2, 1), np.dtype(np.float32)),
+                                  [[3.0, 4.0]])
+
+
 def test_target_normalisation_matches_index_py():
     t = pa.list_(pa.float32(), D)
     q = np.arange(D, dtype=np.float32)

@@ -21,7 +21,7 @@ import pytest
 
 from oracle import oracle as O
 
-NAMES = ["g1_d128", "g1_d768", "g2_ties", "g3_tail", "g4_flight", "g6_fp16"]
+NAMES = ["g1_d128", "g1_d768", "g2_ties", "g3_tail", "g4_flight", "g6_fp16", "g7_nulls"]
 
 
 def fp16_tolerance(ref16, metric, q, x):
@@ -45,7 +45,18 @@ def load(golden_dir, name):
     return z, json.loads(str(z["meta"]))
 
 
+def g7_corpus(meta):
+    """G7 (make_golden.g7_corpus): rows 17 and 1777 planted on queries 0 and 1."""
+    x = O.fill_normal(meta["n"], meta["d"], meta["seed"])
+    q = O.fill_normal(meta["nq"], meta["d"], meta["qseed"])
+    x[17] = q[0]
+    x[1777] = q[1] + np.float32(0.01)
+    return x, q
+
+
 def corpus(meta):
+    if meta["kind"] == "direct_nulls":
+        return g7_corpus(meta)[0]
     if meta.get("dtype") == "float16":
         return O.fill_normal(meta["n"], meta["d"], meta["seed"], dtype=np.float16)
     if meta.get("duplicate"):
@@ -168,3 +179,35 @@ def test_fp16_full_table_matches_reference(golden_dir):
         err = np.abs(o16.astype(np.float64) - ref.astype(np.float64))
         assert np.all(err <= fp16_tolerance(ref, metric, q, x)), metric
         assert (err == 0).mean() > 0.8, metric  # mostly the same half
+
+
+def test_null_slots_scanned_like_reference(golden_dir):
+    """G7: a null slot (validity on the list array, values stored) is scanned
+    and ranked on its stored values; the reference returns it with its
+    distance and a null vector (maxval below the row count: select path;
+    None and above: every row in table order).  The oracle ignores validity
+    exactly like the reference's from_dlpack (io/torch/torch.py:6-10)."""
+    z, meta = load(golden_dir, "g7_nulls")
+    x, q = g7_corpus(meta)
+    nulls = np.array(meta["nulls"])
+    for metric in meta["metrics"]:
+        od, orow = O.knn(x, q, metric, 10)
+        np.testing.assert_array_equal(orow, z[f"{metric}_10_ids"], err_msg=metric)
+        fd = z[f"{metric}_10_dist"].astype(np.float64)
+        # planted near-zero L2 distances: torch.cdist's matmul form cancels
+        # |q|^2 + |x|^2 - 2 q.x, so the bound scales with |q| there
+        qn = np.linalg.norm(q.astype(np.float64), axis=1)[:, None]
+        assert np.all(np.abs(od - fd) <= 1e-5 * np.maximum(np.abs(od), qn)), metric
+        np.testing.assert_array_equal(z[f"{metric}_10_null"], np.isin(orow, nulls))
+        # planted null rows come first for queries 0 and 1
+        assert z[f"{metric}_10_ids"][0, 0] == 17 and z[f"{metric}_10_ids"][1, 0] == 1777
+        ref = O.distances(x, q, metric)
+        scale = {"l2": 20.0, "cosine": 1.0}.get(metric, 150.0)
+        for tag in ("all", "5000"):
+            np.testing.assert_array_equal(z[f"{metric}_{tag}_ids"],
+                                          np.tile(np.arange(meta["n"]), (meta["nq"], 1)))
+            np.testing.assert_array_equal(z[f"{metric}_{tag}_null"][0],
+                                          np.isin(np.arange(meta["n"]), nulls))
+            fd = z[f"{metric}_{tag}_dist"].astype(np.float64)
+            assert np.all(np.abs(ref - fd) <= 1e-5 * np.maximum(np.abs(ref), scale)), metric
+    assert meta["child_nulls_error"].startswith("ArrowTypeError")

@@ -40,14 +40,14 @@ def client(a) -> None:
     rs = np.random.RandomState(1)
     qs = rs.standard_normal((a.reps + 1, a.d)).astype(np.float16 if a.dtype == "f16" else np.float32)
     t0 = time.perf_counter()
-    r = f.search(target=qs[0], source="bench/table", column="vector", metric=a.metric,
+    r = f.search(target=qs[0], source=a.source, column="vector", metric=a.metric,
                  maxval=a.k)
     first = time.perf_counter() - t0
     assert r.num_rows == a.k
     lat = []
     for i in range(a.reps):
         t0 = time.perf_counter()
-        r = f.search(target=qs[i + 1], source="bench/table", column="vector", metric=a.metric,
+        r = f.search(target=qs[i + 1], source=a.source, column="vector", metric=a.metric,
                      maxval=a.k)
         lat.append(time.perf_counter() - t0)
         assert r.num_rows == a.k
@@ -73,6 +73,7 @@ def main() -> None:
                    help="serve every request alone (FENIX_AMD_COALESCE=0)")
     p.add_argument("--client", action="store_true")
     p.add_argument("--port", type=int, default=0)
+    p.add_argument("--source", default="bench/table", help="client: the table to search")
     a = p.parse_args()
     if a.client:
         return client(a)
