@@ -2191,7 +2191,18 @@ __global__ void __launch_bounds__(kI6Threads, 1) filter_img6_kernel(FilterArgs a
     // the partner wave's on the SIMD's matrix pipe).  tools/race_check.py:
     // 0 of 88 repetitions move with it, 201 of 232 without; it costs
     // nothing on a single query (1.295 vs 1.300 ms for configs[1]).
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#ifndef FX_I6_PRE_EPI  // experiment switch (tools/race_check.py builds):
+#define FX_I6_PRE_EPI 1  // 0 no barrier, 1 barrier, 2 own loads drained, 3 64 wait states
+#endif
+    if constexpr (FX_I6_PRE_EPI == 1)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (FX_I6_PRE_EPI == 2)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else if constexpr (FX_I6_PRE_EPI == 3)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" :::
+                   "memory");
+    else
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (!(diag & 2))
       i8_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rext, sh->rrow, sh->rflags, sh->qtab,
                           sh->qinf, a, q0, wid, h, l32, sh->seg, diag);

@@ -2,7 +2,8 @@
 per-query candidate counts compared across repetitions (a count that moves
 means a kernel read data that had not landed).  Prints one line per case.
 
-    python tools/race_check.py [--reps 30]
+    python tools/race_check.py [--reps 30] [--nq 1,2,16,64,65,256] [--img6 0,1,2]
+    FENIX_AMD_LIB=fenix_amd/lib/libfenix_knn_pe0.so python tools/race_check.py ...
 """
 import argparse
 import os
@@ -19,6 +20,9 @@ from tests.test_gpu_kernels import _extreme_rows  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument("--reps", type=int, default=30)
+p.add_argument("--nq", default="1,2,16,64,65,256", help="batch sizes (1-64: the q64i build)")
+p.add_argument("--img6", default="0,1,2", help="option img6 values")
+p.add_argument("--d", default="136,768")
 p.add_argument("--fp16", action="store_true",
                help="the fp16 filter kernels instead: fp16 image (k = 30) and no image (k = 300)")
 a = p.parse_args()
@@ -48,16 +52,16 @@ if a.fp16:
                           + ("no filter" if ref is None else
                              f"{moved} of {a.reps - 1} repetitions moved"), flush=True)
     sys.exit(0)
-for n, d in ((70_000, 136), (70_000, 768)):
+for n, d in [(70_000, int(v)) for v in a.d.split(",")]:
     xh = _extreme_rows(n, d, 49)
     x = torch.from_numpy(xh).to(eng.device)
     eng.clear_images()
     mask = device_mask(np.random.RandomState(4).rand(n) < 0.8, eng.device)
-    for nq in (65, 256):
+    for nq in [int(v) for v in a.nq.split(",")]:
         q = torch.from_numpy(O.fill_normal(nq, d, seed=60 + nq)).to(eng.device)
         for msk in (None, mask):
-            for img6 in (0, 2):
-                with _lib.options(img6=img6, filter_image=8):
+            for img6 in [int(v) for v in a.img6.split(",")]:
+                with _lib.options(img6=img6, filter_image=8, batch_min_queries=1):
                     ref = None
                     moved = 0
                     for _ in range(a.reps):
