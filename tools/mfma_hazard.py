@@ -22,16 +22,17 @@ import re
 import sys
 from collections import deque
 
-REG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+REG = re.compile(r"\b([va])\[(\d+):(\d+)\]|\b([va])(\d+)\b")
 
 
 def regs(text: str):
+    """VGPRs and AGPRs named in an instruction: {("v", 3), ("a", 17), ...}."""
     out = set()
     for m in REG.finditer(text):
         if m.group(1) is not None:
-            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+            out.update((m.group(1), r) for r in range(int(m.group(2)), int(m.group(3)) + 1))
         else:
-            out.add(int(m.group(3)))
+            out.add((m.group(4), int(m.group(5))))
     return out
 
 
