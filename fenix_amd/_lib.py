@@ -80,6 +80,8 @@ SYMBOLS = (
     "fx_mask_compact",
     "fx_knn_search_ex_workspace_bytes",
     "fx_knn_search_ex",
+    "fx_knn_search_shards_workspace_bytes",
+    "fx_knn_search_shards",
     "fx_knn_distances_ex",
     "fx_comm_init_all",
     "fx_comm_destroy",
@@ -223,6 +225,10 @@ def load() -> ctypes.CDLL:
         L.fx_knn_search_ex_workspace_bytes.restype = ci
         L.fx_knn_search_ex.argtypes = [pc_, vp, i64, vp, i64, ci, i64, vp, vp, sz, vp, vp, vp]
         L.fx_knn_search_ex.restype = ci
+        L.fx_knn_search_shards_workspace_bytes.argtypes = [pc_, ci, i64, i64, psz]
+        L.fx_knn_search_shards_workspace_bytes.restype = ci
+        L.fx_knn_search_shards.argtypes = [pc_, ci, vp, i64, ci, i64, vp, vp, sz, vp, vp, vp]
+        L.fx_knn_search_shards.restype = ci
         L.fx_knn_distances_ex.argtypes = [pc_, vp, i64, ci, vp, vp, vp]
         L.fx_knn_distances_ex.restype = ci
         L.fx_comm_init_all.argtypes = [ci, ctypes.POINTER(ci), ctypes.POINTER(vp)]
@@ -354,6 +360,14 @@ def search_ex_workspace_bytes(corpus: "Corpus", nrows: int, nq: int, k: int) -> 
     out = ctypes.c_size_t(0)
     check(load().fx_knn_search_ex_workspace_bytes(ctypes.byref(corpus), nrows, nq, k,
                                                   ctypes.byref(out)))
+    return int(out.value)
+
+
+def search_shards_workspace_bytes(corpora, nq: int, k: int) -> int:
+    """fx_knn_search_shards_workspace_bytes over a ctypes array of Corpus."""
+    out = ctypes.c_size_t(0)
+    check(load().fx_knn_search_shards_workspace_bytes(corpora, len(corpora), nq, k,
+                                                      ctypes.byref(out)))
     return int(out.value)
 
 

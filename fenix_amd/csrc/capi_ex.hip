@@ -3,6 +3,8 @@
 // registers, ex/arrow/quint8/quint8.py:81-84), optional row list and mask.
 // Same plans and kernels as fx_knn_search / fx_knn_search_rows /
 // fx_knn_distances; no batched MFMA path here (it reads f32 rows).
+#include <vector>
+
 #include "fx_internal.h"
 
 namespace fx {
@@ -89,6 +91,57 @@ ScanArgs base_args(const fx_corpus* c, const ScanPlan& p) {
   a.qscale = c->dtype == FX_DTYPE_QU8 ? c->scale : 1.f;
   a.qshift = c->dtype == FX_DTYPE_QU8 ? (float)c->zero_point : 0.f;
   return a;
+}
+
+// fx_knn_search_shards: every shard's scan plan, and where its lists start
+// in the one list buffer [nq][lists][k] the merge reads
+constexpr int kMaxShards = 4096;
+
+struct ShardsPlan {
+  std::vector<ScanPlan> scan;
+  std::vector<int64_t> base;
+  int64_t lists = 0;
+  MergePlan merge;
+  size_t lists_bytes = 0, total = 0;
+};
+
+int check_shards(const fx_corpus* s, int ns, int64_t nq, int64_t k, int metric) {
+  if (s == nullptr || ns < 1 || ns > kMaxShards) {
+    set_error("fx_knn_search_shards: %d shards (1 .. %d)", ns, kMaxShards);
+    return FX_EINVAL;
+  }
+  if (k < 1 || k > kMaxKEx) {
+    set_error("fx_knn_search_shards: k=%lld outside [1, %lld]", (long long)k, (long long)kMaxKEx);
+    return FX_EUNSUPPORTED;
+  }
+  for (int i = 0; i < ns; ++i) {
+    int rc = check_corpus(&s[i], nq, metric);
+    if (rc) return rc;
+    if (s[i].d != s[0].d || s[i].dtype != s[0].dtype) {
+      set_error("fx_knn_search_shards: shard %d has d=%lld dtype %d, shard 0 d=%lld dtype %d", i,
+                (long long)s[i].d, s[i].dtype, (long long)s[0].d, s[0].dtype);
+      return FX_EINVAL;
+    }
+  }
+  return FX_OK;
+}
+
+int plan_shards(const fx_corpus* s, int ns, int64_t nq, int64_t k, int metric, ShardsPlan* p) {
+  p->scan.resize(ns);
+  p->base.resize(ns);
+  p->lists = 0;
+  for (int i = 0; i < ns; ++i) {
+    const bool aligned = ((uintptr_t)s[i].data % 16) == 0;
+    int rc = plan_scan(s[i].n, s[i].d, s[i].dtype, k, metric, aligned, &p->scan[i]);
+    if (rc) return rc;
+    p->base[i] = p->lists;
+    p->lists += p->scan[i].nlists;
+  }
+  int rc = plan_merge(nq, p->lists, k, k, &p->merge);
+  if (rc) return rc;
+  p->lists_bytes = align256((size_t)nq * p->lists * k * 8);
+  p->total = p->lists_bytes + p->merge.ws_bytes;
+  return FX_OK;
 }
 
 }  // namespace
@@ -195,6 +248,64 @@ int fx_knn_distances_ex(const fx_corpus* c, const float* queries, int64_t nq, in
     if (rc) return rc;
   }
   return FX_OK;
+}
+
+int fx_knn_search_shards_workspace_bytes(const fx_corpus* shards, int nshards, int64_t nq,
+                                         int64_t k, size_t* out_bytes) {
+  if (out_bytes == nullptr) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  int rc = check_shards(shards, nshards, nq, k, FX_METRIC_L2);
+  if (rc) return rc;
+  size_t best = 0;
+  for (int metric = FX_METRIC_L2; metric <= FX_METRIC_COS; ++metric) {  // (plans are per metric)
+    ShardsPlan p;
+    rc = plan_shards(shards, nshards, nq, k, metric, &p);
+    if (rc) return rc;
+    if (p.total > best) best = p.total;
+  }
+  *out_bytes = best;
+  return FX_OK;
+}
+
+int fx_knn_search_shards(const fx_corpus* shards, int nshards, const float* queries, int64_t nq,
+                         int metric, int64_t k, const uint32_t* const* masks, void* ws,
+                         size_t ws_bytes, float* out_dist, int64_t* out_row, void* stream) {
+  int rc = check_shards(shards, nshards, nq, k, metric);
+  if (rc) return rc;
+  if (!queries || !ws || !out_dist || !out_row) {
+    set_error("null pointer argument");
+    return FX_EINVAL;
+  }
+  ShardsPlan p;
+  rc = plan_shards(shards, nshards, nq, k, metric, &p);
+  if (rc) return rc;
+  if (ws_bytes < p.total) {
+    set_error("workspace too small: %zu < %zu", ws_bytes, p.total);
+    return FX_EINVAL;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  uint64_t* lists = reinterpret_cast<uint64_t*>(ws);
+  const int64_t d = shards[0].d;
+  for (int i = 0; i < nshards; ++i) {
+    ScanArgs a = base_args(&shards[i], p.scan[i]);
+    a.n = shards[i].n;
+    a.mask = masks != nullptr ? masks[i] : nullptr;
+    a.k = (int)k;
+    a.mode = kModeTopk;
+    a.list_stride = p.lists;
+    a.list_base = p.base[i];
+    for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
+      const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
+      a.q = queries + (size_t)q0 * d;
+      a.out_lists = lists + (size_t)q0 * p.lists * k;
+      rc = launch_scan(p.scan[i], a, qn, st);
+      if (rc) return rc;
+    }
+  }
+  return run_merge(p.merge, lists, nq, k, reinterpret_cast<char*>(ws) + p.lists_bytes, out_dist,
+                   out_row, st);
 }
 
 }  // extern "C"

@@ -56,7 +56,10 @@ struct ScanArgs {
   int cap;                // per-wave candidate list capacity
   size_t qbytes;          // LDS bytes reserved for the query
   int mode;               // kModeTopk / kModeDist
-  uint64_t* out_lists;    // topk: [nq][gridDim.x][k] composites (one list per block)
+  uint64_t* out_lists;    // topk: [nq][list_stride][k] composites (one list per block,
+                          // block b at list list_base + b)
+  int64_t list_stride;    // lists per query in out_lists (0: gridDim.x)
+  int64_t list_base;      // this launch's first list (fx_knn_search_shards: the shard's)
   float* out_dist;        // dist: [nq][n]
   float qscale, qshift;   // FX_DTYPE_QU8: value = qscale * (code - qshift)
   // bit 0 clear: block b scans rows [b * rows_per_block, ...) in order; set:

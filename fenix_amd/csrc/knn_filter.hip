@@ -2055,6 +2055,13 @@ __global__ void __launch_bounds__(kI6Threads, 1) filter_img6_kernel(FilterArgs a
   const int64_t ntile32 = (a.n + 31) / 32;
   const int64_t ntiles = a.num_tiles;
   if ((int64_t)blockIdx.x >= ntiles) return;
+  if (a.skip_full) {  // every query of the slice predicted to overflow (the gate): the
+                      // exact scan recomputes them, so the final pass has nothing to do
+    bool full = true;
+    for (int q = tid; q < fBQ; q += kI6Threads)
+      if (q0 + q < a.nq && a.count[(q0 + q) * kCountStride] <= (uint32_t)a.cap) full = false;
+    if (__syncthreads_and(full)) return;
+  }
   i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, kI6Threads);
   for (int q = tid; q < fBQ; q += kI6Threads) sh->seg[q] = 0u;
   {  // the slice: chunk c of query Q at (c * 128 + Q) * 64, piece p at (p ^ ((Q >> 2) & 3)) * 16

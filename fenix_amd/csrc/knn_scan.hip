@@ -677,7 +677,8 @@ __global__ void __launch_bounds__(256, kMinWaves<T>) scan_kernel(ScanArgs a) {
   __syncthreads();
   block_or_and(v_or, v_and, ms);
   __syncthreads();
-  uint64_t* out = a.out_lists + ((size_t)qi * gridDim.x + blockIdx.x) * (size_t)a.k;
+  const size_t ls = a.list_stride > 0 ? (size_t)a.list_stride : (size_t)gridDim.x;
+  uint64_t* out = a.out_lists + ((size_t)qi * ls + a.list_base + blockIdx.x) * (size_t)a.k;
   block_keep_k<256>(all, 4 * a.k, a.k, out, ms);
 }
 

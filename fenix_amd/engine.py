@@ -699,6 +699,42 @@ class Engine:
             return
         self.search_shard(shard, queries, metric, k, mask, out_dist, out_row)
 
+    # several exact-scan shards on this device share one merge tree
+    # (fx_knn_search_shards); False: a merge per shard, then one over them
+    ONE_MERGE = True
+
+    def _one_merge(self, shards: Sequence[Shard], nq: int, k: int, metric: int,
+                   masks: Optional[Sequence[Optional[torch.Tensor]]]) -> bool:
+        """fx_knn_search_shards applies: a single query whose every shard
+        takes the exact scan (no filter image, k within the fused scan's),
+        no masks (a mask may pick the row-list scan per shard), one d and
+        dtype."""
+        if not self.ONE_MERGE or nq != 1 or k > _lib.max_k():
+            return False
+        if masks is not None and any(m is not None for m in masks):
+            return False
+        d, dt = shards[0].d, shards[0].dtype_id
+        for s in shards:
+            if s.d != d or s.dtype_id != dt or s.n < 1:
+                return False
+            if dt != _lib.DTYPE_QU8 and _lib.filter_image_used(s.n, s.d, dt, nq, k, metric):
+                return False
+        return True
+
+    def _search_shards(self, shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: int,
+                       out_dist: torch.Tensor, out_row: torch.Tensor) -> None:
+        """fx_knn_search_shards: every shard's scan into one list buffer, one
+        merge; caller holds lock."""
+        arr = (_lib.Corpus * len(shards))(*[s.corpus() for s in shards])
+        key = ("shards", self.device.index, queries.shape[0], k,
+               tuple((s.n, s.d, s.dtype_id, s.data.data_ptr() % 16 == 0) for s in shards))
+        ws = self._workspace(_lib._planned(
+            key, lambda: _lib.search_shards_workspace_bytes(arr, queries.shape[0], k)))
+        self._hold(*[s.data for s in shards])
+        _lib.check(_lib.load().fx_knn_search_shards(
+            arr, len(shards), _ptr(queries), queries.shape[0], metric, k, None, _ptr(ws),
+            ws.numel(), _ptr(out_dist), _ptr(out_row), self._stream()))
+
     def search(self, shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: int,
                masks: Optional[Sequence[Optional[torch.Tensor]]] = None,
                counts: Optional[Sequence[Optional[int]]] = None,
@@ -714,6 +750,11 @@ class Engine:
                 od = torch.empty((nq, k), dtype=torch.float32, device=self.device)
                 orow = torch.empty((nq, k), dtype=torch.int64, device=self.device)
                 self._search_one(shards[0], queries, metric, k, mask_of(0), count_of(0), od, orow)
+                return od, orow
+            if self._one_merge(shards, nq, k, metric, masks):
+                od = torch.empty((nq, k), dtype=torch.float32, device=self.device)
+                orow = torch.empty((nq, k), dtype=torch.int64, device=self.device)
+                self._search_shards(shards, queries, metric, k, od, orow)
                 return od, orow
             pd = torch.empty((nq, len(shards), k), dtype=torch.float32, device=self.device)
             pr = torch.empty((nq, len(shards), k), dtype=torch.int64, device=self.device)

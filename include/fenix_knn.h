@@ -415,6 +415,25 @@ typedef struct fx_corpus {
   int32_t zero_point;  /* QU8 only */
 } fx_corpus;
 
+/*
+ * Exact top-k over several row shards that live on ONE device (the sources
+ * of a multi-source table, table.py:19-21, or several shards of one column
+ * on one GPU) with ONE merge tree: every shard's fused scan writes its
+ * per-block top-k lists into one buffer and a single merge selects the k
+ * smallest (distance, global row) over all of them.  The per-shard form
+ * (fx_knn_search per shard + fx_topk_merge) runs a merge tree per shard and
+ * one more over the shards.  Replaces index.py:162-168 over concatenated
+ * sources.  Shards: same d, dtype FX_DTYPE_F32 or FX_DTYPE_F16, n >= 1,
+ * each with its own row_base; masks: NULL, or one bitmap (or NULL) per
+ * shard.  k <= fx_max_k().  Exact scan only (a caller with a filter image
+ * keeps the per-shard calls).  Results equal the per-shard form bit for bit.
+ */
+int fx_knn_search_shards_workspace_bytes(const fx_corpus* shards, int nshards, int64_t nq,
+                                         int64_t k, size_t* out_bytes);
+int fx_knn_search_shards(const fx_corpus* shards, int nshards, const float* queries, int64_t nq,
+                         int metric, int64_t k, const uint32_t* const* masks, void* ws,
+                         size_t ws_bytes, float* out_dist, int64_t* out_row, void* stream);
+
 int fx_knn_search_ex_workspace_bytes(const fx_corpus* c, int64_t nrows, int64_t nq, int64_t k,
                                      size_t* out_bytes);
 int fx_knn_search_ex(const fx_corpus* c, const int32_t* rows, int64_t nrows,

@@ -1089,3 +1089,50 @@ def test_interleaved_scan_equals_contiguous(eng, n, d, dtype, metric):
                        dtype=np.float32 if dtype == torch.float32 else np.float16).astype(np.float32)
     od, orow = O.knn(xh, q.cpu().numpy(), metric, k)
     check_topk(ref[0][0], ref[0][1] - 11, od, orow, xh, q.cpu().numpy(), metric)
+
+
+# ---------------------------------------- several shards on one device, one merge
+
+
+@pytest.mark.parametrize("metric", METRICS)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_search_shards_one_merge_equals_per_shard(eng, metric, dtype):
+    """fx_knn_search_shards (every shard's scan into one list buffer, ONE
+    merge tree) returns the per-shard form's bits (a merge per shard, then
+    fx_topk_merge over the shards), and the oracle's rows: shards of uneven
+    sizes, one smaller than k, one 4 bytes off 16-byte alignment (the
+    scalar-load scan), row bases with gaps (global rows of the sources as
+    numbered by table.py:19-21), k from 10 to the fused scan's 1 024."""
+    d = 136
+    sizes = [50_000, 777, 20_000, 3_001]
+    xs, shards, base = [], [], 0
+    for i, n in enumerate(sizes):
+        x = gpu_fill(eng, n + (1 if i == 2 else 0), d, seed=80 + i, dtype=dtype)
+        if i == 2:  # a view 1 row + 4 bytes in: not 16-B aligned
+            flat = x.view(-1)[1 : 1 + n * d] if dtype == torch.float32 else x.view(-1)[2 : 2 + n * d]
+            x = flat.view(n, d)
+            assert x.data_ptr() % 16 != 0
+        xs.append(x.float().cpu().numpy())
+        shards.append(Shard(x, base))
+        base += n + 1000 * (i + 1)  # gaps between the sources' global rows
+    q = torch.from_numpy(O.fill_normal(1, d, seed=90))
+    m = _lib.METRICS[metric]
+    for k in (10, 100, 1000, 1024):
+        assert eng._one_merge(shards, 1, k, m, None)
+        one = eng.search(shards, q, m, k)
+        Engine.ONE_MERGE = False
+        try:
+            per = eng.search(shards, q, m, k)
+        finally:
+            Engine.ONE_MERGE = True
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(one[1].cpu().numpy(), per[1].cpu().numpy())
+        np.testing.assert_array_equal(one[0].cpu().numpy().view(np.uint32),
+                                      per[0].cpu().numpy().view(np.uint32))
+    # the rows against the float64 oracle over the concatenated sources
+    allx = np.concatenate(xs)
+    glob = np.concatenate([s.row_base + np.arange(s.n) for s in shards])
+    od, orow = O.knn(allx, q.numpy(), metric, 100)
+    gd, gr = eng.search(shards, q, m, 100)
+    # (global rows increase with the concatenated index: the same tie order)
+    check_topk(gd.cpu().numpy(), gr.cpu().numpy(), od, glob[orow], allx, q.numpy(), metric)
