@@ -1171,6 +1171,10 @@ static int launch_img2(const FilterArgs& a, int metric, hipStream_t stream) {
 #define FX_I3_XPF 0   // 1: the next tile's first image chunks in flight during the
                       // epilogue (equal with 4 stages, 1-2 % faster with 2)
 #endif
+#ifndef FX_I3_PAIR
+#define FX_I3_PAIR 1  // 1: the ring refilled two chunks at a time, one barrier per
+                      // two steps (the ring then holds two pairs; FX_I3_QA unused)
+#endif
 #ifndef FX_I3_WAVES
 #define FX_I3_WAVES 8  // waves per workgroup: 8 (one 256-row workgroup per CU) or 4
                        // (two independent 128-row workgroups per CU)
@@ -1809,8 +1813,9 @@ __global__ void __launch_bounds__(kI3Threads, 2) filter_img3_kernel(FilterArgs a
   // ---- prologue: query chunks 0 .. QA-1 and image chunks 0 .. XS-1 of the
   // first tile in flight
   int qc = 0, qslot = 0;  // next query chunk to issue and its slot
+  static_assert(!FX_I3_PAIR || (kI3Slots == 4 && XS % 2 == 0), "FX_I3_PAIR: two pairs, even stages");
 #pragma unroll
-  for (int i = 0; i < FX_I3_QA; ++i) {
+  for (int i = 0; i < (FX_I3_PAIR ? 2 : FX_I3_QA); ++i) {
     issue_q(qc, qslot);
     qc = qc + 1 == nch ? 0 : qc + 1;
     qslot = qslot + 1 == kI3Slots ? 0 : qslot + 1;
@@ -1849,6 +1854,26 @@ __global__ void __launch_bounds__(kI3Threads, 2) filter_img3_kernel(FilterArgs a
       // terms, only make the wait stronger), and every wave done with the
       // slot refilled next
       constexpr bool LD = decltype(ld)::value;
+      if constexpr (FX_I3_PAIR) {
+        // even steps only (nch is a multiple of XS, so the step parity is
+        // S's): the pair (c + S, c + S + 1) was issued two steps back, and
+        // after it only image chunks: the two steps' own (none in a tile's
+        // last group), or at a tile's first group the post-epilogue stages
+        if constexpr (S % 2 == 0) {
+          constexpr int kN = S == 0 ? (decltype(first)::value && !FX_I3_XPF ? XS * kI2KS : 2 * kI2KS)
+                                    : (LD ? 2 * kI2KS : 0);
+          if (diag & 16)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          else
+            i3_wait_barrier<kN>();
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {  // into the pair every wave finished before the barrier
+            issue_q(qc, qslot);
+            qc = qc + 1 == nch ? 0 : qc + 1;
+            qslot = qslot + 1 == kI3Slots ? 0 : qslot + 1;
+          }
+        }
+      } else {
       constexpr int kXAfter = LD ? FX_I3_QA : (FX_I3_QA > S ? FX_I3_QA - S : 0);
       if (diag & 16)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1857,6 +1882,7 @@ __global__ void __launch_bounds__(kI3Threads, 2) filter_img3_kernel(FilterArgs a
       issue_q(qc, qslot);
       qc = qc + 1 == nch ? 0 : qc + 1;
       qslot = qslot + 1 == kI3Slots ? 0 : qslot + 1;
+      }
       if constexpr (decltype(first)::value && S == 0) {  // the rows' image sums and mask words of this tile
         const int64_t row = r0 + lr < a.n ? r0 + lr : a.n - 1;
         if constexpr (I8)
