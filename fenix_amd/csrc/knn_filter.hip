@@ -2015,6 +2015,421 @@ static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
   return check_launch("filter_img3_kernel");
 }
 
+#if FX_FILTER_BQ >= 256
+// ---- int8 image, the queries held in registers (filter_img8_kernel)
+//
+// filter_img3_kernel keeps each wave's image rows in registers and streams
+// the 256-query tile through LDS: every 64-component chunk of every 256-row
+// tile DMAs the queries again from L2, as many bytes as the image itself
+// (without those DMAs the final pass ran 25 % faster).  Here
+// the operands swap roles: wave w holds queries 32 w .. 32 w + 31 as MFMA A
+// operands for every k-step (24 x 16 B per lane: d <= 768) for the whole
+// kernel, and the image goes through a 4-slot LDS ring by DMA straight from
+// HBM (16 KB chunks: 128 rows x 4 k-steps, each 32-row k-step one contiguous
+// KB in the image's fragment order, read back as the B operand with one
+// conflict-free ds_read_b128).  The only bytes that move are the image's,
+// once.  The accumulator of a (32-query, 32-row) tile then holds one row per
+// lane and 16 queries: the pass test is i8_epilogue's with the pairs taken
+// over queries instead of rows (the same f32 operations per (row, query)
+// pair: bit-identical decisions), appends one LDS atomic per passing pair.
+// Serves 256-query batches (not all-pass) of int8 images with d <= 768.
+#ifndef FX_I8T
+#define FX_I8T 1
+#endif
+#ifndef FX_T8_SLOTS
+#define FX_T8_SLOTS 4  // ring slots of 16 KB (FX_T8_SLOTS - 1 chunks in flight)
+#endif
+#ifndef FX_T8_SEG
+#define FX_T8_SEG 24   // LDS append entries per query (overflow: global slots)
+#endif
+#ifndef FX_T8_PAIR
+#define FX_T8_PAIR 1   // 1: the ring refilled two chunks at a time, one barrier per two
+                       // chunks (an even chunk count per tile; FX_T8_SLOTS even)
+#endif
+#ifndef FX_T8_PRIO
+#define FX_T8_PRIO 0   // 1: waves 4-7 (each SIMD's second wave) at s_setprio 1
+#endif
+constexpr int kT8Waves = 8;
+constexpr int kT8Threads = 64 * kT8Waves;
+constexpr int kT8BM = 128;                            // rows per workgroup tile
+constexpr int kT8RT = kT8BM / 32;                     // 32-row tiles (B operands)
+constexpr int kT8Sub = fBM / kT8BM;                   // workgroup tiles per plan tile
+constexpr int kT8KS = 24;                             // k-steps in registers (d <= 768)
+constexpr int kT8CK = 4;                              // k-steps per ring chunk
+constexpr int kT8NC = kT8KS / kT8CK;                  // ring chunks per tile, at most
+constexpr int kT8SlotBytes = kT8RT * kT8CK * 1024;    // 16 KB
+constexpr int kT8Slots = FX_T8_SLOTS;
+constexpr int kT8QA = kT8Slots - 1;                   // chunks in flight
+constexpr int kT8Dma = kT8SlotBytes / 1024 / kT8Waves;  // 1-KB DMAs per wave per chunk
+constexpr int kT8SEG = FX_T8_SEG;
+static_assert(kT8Waves * 32 == fBQ && kT8Sub * kT8BM == fBM && kT8Dma == 2 &&
+                  kT8RT * kT8CK == kT8Waves * kT8Dma,
+              "filter_img8_kernel tiling");
+struct Img8Shared {
+  unsigned char ring[kT8Slots][kT8SlotBytes];
+  float rinfo[kT8BM];   // omega (NaN: forced)
+  float rterm[kT8BM];   // y1
+  float rext[kT8BM];    // 1 / s
+  uint32_t rrow[kT8BM];   // the global corpus row (image8_perm)
+  uint32_t rkeep[kT8BM];  // 1: a row in range and not masked out
+  f32x4 qtab[fBQ];
+  f32x4 qinf[fBQ];
+  uint32_t seg[fBQ + 3 * fBQ * kT8SEG];
+  uint32_t segbase[fBQ];
+};
+static_assert(sizeof(Img8Shared) <= 160 * 1024, "filter_img8_kernel: LDS over 160 KB");
+
+// Pass test and appends of one wave's (32 queries x 128 rows) accumulators:
+// acc[t] element j is row 32 t + l32 against query 32 wid + (j & 3) + 8 (j >> 2) + 4 h.
+template <int METRIC>
+__device__ __forceinline__ void t8_epilogue(const f32x16 (&acc)[kT8RT], const Img8Shared* sh,
+                                            uint32_t* seg, const FilterArgs& a, int64_t q0,
+                                            int wid, int h, int l32) {
+  constexpr int SEG = kT8SEG;
+  float om[kT8RT], y1[kT8RT], y2[kT8RT];
+  uint32_t keep[kT8RT];
+#pragma unroll
+  for (int t = 0; t < kT8RT; ++t) {
+    const int lr = t * 32 + l32;
+    om[t] = sh->rinfo[lr];
+    y1[t] = sh->rterm[lr];
+    y2[t] = METRIC == 0 ? sh->rext[lr] : 0.f;
+    keep[t] = sh->rkeep[lr] ? 0xffffu : 0u;
+  }
+  const int qb = wid * 32 + 4 * h;  // query of element j: qb + (j & 3) + 8 (j >> 2)
+  uint32_t qlive = 0u;
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    qlive |= (q0 + qb + (j & 3) + 8 * (j >> 2) < a.nq ? 1u : 0u) << j;
+  // fail bit j enters last-in at bit 0: pairs (j, j + 1) run down
+  uint32_t fail[kT8RT];
+#pragma unroll
+  for (int t = 0; t < kT8RT; ++t) fail[t] = 0u;
+  const f32x2 nc0 = {-kI8C0, -kI8C0};
+#pragma unroll
+  for (int jp = 7; jp >= 0; --jp) {
+    const int j = 2 * jp;
+    const int q = qb + (j & 3) + 8 * (j >> 2);  // queries q, q + 1
+    const f32x4 ca = sh->qtab[q], cb = sh->qtab[q + 1];
+    const f32x2 ra = {ca[0], cb[0]}, c1 = {ca[1], cb[1]}, c2 = {ca[2], cb[2]};
+#pragma unroll
+    for (int t = 0; t < kT8RT; ++t) {
+      const f32x2 xp = {acc[t][j], acc[t][j + 1]};
+      f32x2 v = __builtin_elementwise_fma(f32x2{om[t], om[t]}, ra, xp);
+      v = __builtin_elementwise_fma(f32x2{y1[t], y1[t]}, c1, v);
+      if constexpr (METRIC == 0) v = __builtin_elementwise_fma(f32x2{y2[t], y2[t]}, c2, v);
+      const f32x2 dd = v + nc0;
+      fail[t] = __builtin_amdgcn_alignbit(fail[t], __float_as_uint(dd[1]), 31);
+      fail[t] = __builtin_amdgcn_alignbit(fail[t], __float_as_uint(dd[0]), 31);
+    }
+  }
+  uint32_t pm[kT8RT], any = 0u;
+#pragma unroll
+  for (int t = 0; t < kT8RT; ++t) {
+    const uint32_t force = om[t] != om[t] ? ~0u : 0u;  // a forced row passes every query
+    pm[t] = (~fail[t] | force) & keep[t] & qlive;
+    any |= pm[t];
+  }
+  if (__ballot(any != 0u) == 0ull) return;
+  static_for<kT8RT>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    uint32_t bits = pm[t];
+    if (__ballot(bits != 0u) == 0ull) return;
+    const int lr = t * 32 + (int)opaque((unsigned)l32);
+    const float ys = sh->rext[lr];
+    const uint32_t grow = sh->rrow[lr];
+    while (bits != 0u) {
+      const int j = __builtin_ctz(bits);
+      bits &= bits - 1u;
+      auto pick = [](float lo, float hi, uint32_t m) {
+        return __uint_as_float((__float_as_uint(hi) & m) | (__float_as_uint(lo) & ~m));
+      };
+      const uint32_t m0 = 0u - ((uint32_t)j & 1u), m1 = 0u - (((uint32_t)j >> 1) & 1u);
+      const uint32_t m2 = 0u - (((uint32_t)j >> 2) & 1u), m3 = 0u - (((uint32_t)j >> 3) & 1u);
+      float v8[8], v4[4], v2[2];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v8[i] = pick(acc[t][2 * i], acc[t][2 * i + 1], m0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v4[i] = pick(v8[2 * i], v8[2 * i + 1], m1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) v2[i] = pick(v4[2 * i], v4[2 * i + 1], m2);
+      const float x = pick(v2[0], v2[1], m3);
+      const int qi = qb + (j & 3) + 8 * (j >> 2);
+      const int64_t gq = q0 + qi;
+      float lb, ub;
+      i8_bounds<METRIC>(x, om[t], y1[t], ys, sh->qinf[qi], a.d, lb, ub);
+      const uint32_t p = atomicAdd(&seg[qi], 1u);
+      if (p < (uint32_t)SEG) {
+        uint32_t* e = seg + fBQ + 3 * (qi * SEG + p);
+        e[0] = order_key(lb);
+        e[1] = order_key(ub);
+        e[2] = grow;
+      } else {  // rare: past the segment, a global slot
+        const uint32_t gp = atomicAdd(&a.count[gq * kCountStride], 1u);
+        if (gp < (uint32_t)a.cap) {
+          const size_t slot = (size_t)gq * a.cap + gp;
+          if (a.cand_ub != nullptr) {
+            a.cand[slot] = make_comp(lb, grow);
+            a.cand_ub[slot] = make_comp(ub, grow);
+          } else {
+            a.cand[slot] = make_comp(ub, grow);
+          }
+        }
+      }
+    }
+  });
+}
+
+// NCH: ring chunks per tile, ceil(ceil(d / 32) / 4) (a compile-time chunk
+// loop: straight-line code, where the compiler counts every wait exactly)
+template <int METRIC, int NCH>
+__global__ void __launch_bounds__(kT8Threads, 2) filter_img8_kernel(FilterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Img8Shared* sh = reinterpret_cast<Img8Shared*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, l32 = lane & 31;
+  const int64_t q0 = (int64_t)blockIdx.y * fBQ;
+  const int ksteps = (a.d + 31) / 32;  // the image's k-steps per 32-row tile (<= 4 NCH)
+  constexpr int nch = NCH;
+  static_assert(NCH >= 1 && NCH <= kT8NC, "filter_img8_kernel: d <= 768");
+  const int64_t ntile32 = (a.n + 31) / 32;
+  const int64_t ntiles = a.num_tiles * kT8Sub;
+  auto tile_r0 = [&](int64_t ti) {
+    return (a.tile_start + (ti / kT8Sub) * a.tile_stride) * fBM + (ti % kT8Sub) * kT8BM;
+  };
+  if ((int64_t)blockIdx.x >= ntiles) return;
+  if (a.skip_full) {  // every query of the tile predicted to overflow: nothing to do
+    bool full = true;
+    for (int q = tid; q < fBQ; q += kT8Threads)
+      if (q0 + q < a.nq && a.count[(q0 + q) * kCountStride] <= (uint32_t)a.cap) full = false;
+    if (__syncthreads_and(full)) return;
+  }
+  i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, kT8Threads);
+  for (int q = tid; q < fBQ; q += kT8Threads) sh->seg[q] = 0u;
+  // the wave's 32 queries, every k-step: chunk c of query q is 64 B at
+  // (c * qstride + q) * 64 (qprep8), k-step s its half s & 1 (zeros past dq)
+  i32x4 qa[kT8KS];
+  {
+    const unsigned char* qb = reinterpret_cast<const unsigned char*>(a.Qh + q0 * 32);
+    const int qchunks = a.dq / 64;
+    const int64_t qo = (int64_t)(wid * 32 + l32) * 64 + h * 16;
+#pragma unroll
+    for (int s = 0; s < kT8KS; ++s) {
+      const int c = s >> 1;
+      qa[s] = c < qchunks ? *reinterpret_cast<const i32x4*>(qb + (int64_t)c * a.qstride * 64 + qo +
+                                                             (s & 1) * 32)
+                          : i32x4(0);
+    }
+  }
+  __syncthreads();
+
+  // the ring: chunk c of a tile holds its 4 32-row tiles x k-steps 4 c .. 4 c
+  // + 3, KB (tt, kk) at (4 tt + kk) KB; wave w DMAs tile tt = w / 2, k-steps
+  // 2 (w & 1), + 1 (past ksteps: dropped, the slot keeps an earlier chunk's
+  // finite bytes, multiplied by zero query k-steps; past the rows: an empty
+  // descriptor, rows the epilogue skips)
+  const int tt = wid >> 1, kk0 = (wid & 1) * 2;
+  auto x_rsrc = [&](int64_t ti) {
+    const int64_t t32 = tile_r0(ti) / 32 + tt;
+    const int64_t live = (ti < ntiles && t32 < ntile32) ? 1 : 0;
+    const unsigned char* base = reinterpret_cast<const unsigned char*>(a.X) +
+                                (live ? t32 : 0) * (int64_t)ksteps * 1024;
+    const uint64_t xp = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xp);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xp >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)(live * ksteps * 1024));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             nb, 0x00020000);
+  };
+  const uint32_t xl = (uint32_t)opaque((unsigned)lane) * 16u;
+  int64_t xt = blockIdx.x;  // tile and chunk of the next DMA
+  int xc = 0, wslot = 0;
+  __amdgpu_buffer_rsrc_t xr = x_rsrc(xt);
+  auto issue = [&]() {
+    unsigned char* st = sh->ring[wslot] + (tt * kT8CK + kk0) * 1024;
+#pragma unroll
+    for (int i = 0; i < kT8Dma; ++i) {
+      const int s = xc * kT8CK + kk0 + i;  // (wave-uniform)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (i3_lds_ptr)(st + i * 1024), 16,
+                                               s < ksteps ? xl : 0x7fff0000u, s * 1024, 0, 0);
+    }
+    if (++xc == nch) {
+      xc = 0;
+      xt += gridDim.x;
+      xr = x_rsrc(xt);
+    }
+    wslot = wslot + 1 == kT8Slots ? 0 : wslot + 1;
+  };
+  // (pairs: the ring holds kT8Slots / 2 pairs, all but one in flight)
+  constexpr bool PAIR = FX_T8_PAIR && NCH % 2 == 0;
+  static_assert(!FX_T8_PAIR || kT8Slots % 2 == 0, "FX_T8_PAIR: an even ring");
+  constexpr int kAhead = PAIR ? kT8Slots - 2 : kT8QA;  // chunks issued ahead of the one read
+#pragma unroll
+  for (int i = 0; i < kAhead; ++i) issue();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (once: the query fragments too)
+
+  f32x16 acc[kT8RT];
+  const f32x16 acc0 = f32x16(kI8Magic);  // see "int8 filter image"
+  int rslot = 0;
+  if (FX_T8_PRIO && wid >= 4) __builtin_amdgcn_s_setprio(1);
+  const int lr = tid & (kT8BM - 1);  // the row this thread notes (threads >= kT8BM: duplicates)
+  for (int64_t ti = blockIdx.x; ti < ntiles; ti += gridDim.x) {
+    const int64_t r0 = tile_r0(ti);
+    f32x4 rsum = {};
+    uint32_t mword = ~0u;  // (no mask: every row)
+    static_for<NCH>([&](auto cc) {
+      constexpr int C = decltype(cc)::value;
+      // chunk C landed: after its DMAs this wave issued QA - 1 chunks' DMAs
+      // (and possibly the rows' terms: a stronger wait), and every wave is
+      // done with the slot refilled next
+      if constexpr (PAIR) {
+        // even chunks only: the pair (C, C + 1) landed (after its DMAs this
+        // wave issued the kAhead / 2 - 1 pairs ahead of it), every wave done
+        // with the pair refilled next
+        if constexpr (C % 2 == 0) {
+          i3_wait_barrier<(kAhead - 2) * kT8Dma>();
+          issue();
+          issue();
+        }
+      } else {
+        i3_wait_barrier<(kT8QA - 1) * kT8Dma>();
+        issue();
+      }
+      if constexpr (C == 0) {  // the rows' terms and mask words of this tile
+        const int64_t row = r0 + lr < a.n ? r0 + lr : a.n - 1;
+        rsum = *reinterpret_cast<const f32x4*>(a.rowinfo + row * kI8RowInfo);
+        // (used at the tile's last chunk; no load without a mask: a load of
+        // the row's terms there was merged with rsum's, and waited for here)
+        if (a.mask != nullptr) mword = a.mask[perm_row(a.perm_a, a.n, row) >> 5];
+      }
+      // the k-steps of this barrier interval (chunks C .. C + G - 1) in one
+      // stream, B fragments read two k-steps ahead: k-step j + 2's reads
+      // issue before k-step j's MFMAs, across the pair's chunk boundary too
+      constexpr int G = PAIR ? 2 : 1;
+      if constexpr (C % G == 0) {
+        constexpr int J = G * kT8CK;
+        typedef int i32x16 __attribute__((ext_vector_type(16)));
+        auto read_b = [&](i32x4 (&b)[kT8RT], auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const int slot = rslot + j / kT8CK < kT8Slots ? rslot + j / kT8CK : rslot + j / kT8CK - kT8Slots;
+          const unsigned char* st = sh->ring[slot] + lane * 16 + (j % kT8CK) * 1024;
+#pragma unroll
+          for (int t = 0; t < kT8RT; ++t) b[t] = *reinterpret_cast<const i32x4*>(st + t * kT8CK * 1024);
+        };
+        auto mfma4 = [&](const i32x4 (&b)[kT8RT], auto jc) {
+          constexpr int j = decltype(jc)::value;
+          constexpr int s = (C + j / kT8CK) * kT8CK + j % kT8CK;  // the query k-step
+#pragma unroll
+          for (int t = 0; t < kT8RT; ++t) {
+            const f32x16 cin = s == 0 ? acc0 : acc[t];
+            acc[t] = __builtin_bit_cast(
+                f32x16, __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], b[t],
+                                                              __builtin_bit_cast(i32x16, cin), 0, 0, 0));
+          }
+        };
+        i32x4 b0[kT8RT], b1[kT8RT];
+        read_b(b0, std::integral_constant<int, 0>{});
+        read_b(b1, std::integral_constant<int, 1>{});
+        __builtin_amdgcn_sched_barrier(0);
+        static_for<J>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          if constexpr (j % 2 == 0)
+            mfma4(b0, jc);
+          else
+            mfma4(b1, jc);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (j + 2 < J) {
+            if constexpr (j % 2 == 0)
+              read_b(b0, std::integral_constant<int, j + 2>{});
+            else
+              read_b(b1, std::integral_constant<int, j + 2>{});
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        });
+        rslot = rslot + G < kT8Slots ? rslot + G : rslot + G - kT8Slots;
+      }
+      // one thread per row notes its terms for the epilogue, after the last
+      // chunk's MFMAs: in this unrolled straight line the compiler counts
+      // the exact wait for the terms' loads (landed by now: they retire
+      // before the chunk waits of steps 3 on), where after the loop it
+      // could only wait vmcnt(0), for the next tile's DMAs too (the rows of
+      // the previous tile's epilogue were read before this tile's first barrier)
+      if (C == NCH - 1 && tid < kT8BM) {
+        const int lr = (int)opaque((unsigned)tid);
+        const int64_t row = r0 + lr;
+        const int64_t mrow = perm_row(a.perm_a, a.n, row < a.n ? row : a.n - 1);
+        const bool ok = row < a.n && ((mword >> (mrow & 31)) & 1u);
+        // (every lane of the terms' load stays live to here: a dead one was
+        // reused for the mask word, whose write then waited for the load)
+        asm volatile("" ::"v"(rsum[0]), "v"(rsum[1]), "v"(rsum[2]), "v"(rsum[3]));
+        sh->rinfo[lr] = rsum[0];
+        sh->rterm[lr] = METRIC == 1 ? rsum[1] : METRIC == 2 ? rsum[2] : rsum[3];
+        sh->rext[lr] = rsum[1];
+        sh->rrow[lr] = (uint32_t)a.row_base + (row < a.n ? (uint32_t)mrow : 0u);
+        sh->rkeep[lr] = ok ? 1u : 0u;
+      }
+    });
+    // (the barrier also separates the tile's last MFMAs from the epilogue's
+    // reads of their accumulators)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    t8_epilogue<METRIC>(acc, sh, sh->seg, a, q0, wid, h, l32);
+  }
+  // the ring's last DMAs (past the end) land before the workgroup's LDS is
+  // released; then the segments go out
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  filter_flush_segments<kT8SEG, kT8Threads>(sh->seg, sh->segbase, a, q0, tid);
+}
+
+static bool img8_serves(const FilterArgs& a) {
+  return FX_I8T && a.img8 && !a.all_pass && a.dq <= kT8KS * 32 && (a.d + 31) / 32 <= kT8KS;
+}
+
+template <int NCH>
+static const void* img8_fn(int metric) {
+  return metric == FX_METRIC_COS  ? (const void*)filter_img8_kernel<2, NCH>
+         : metric == FX_METRIC_IP ? (const void*)filter_img8_kernel<1, NCH>
+                                  : (const void*)filter_img8_kernel<0, NCH>;
+}
+
+static int launch_img8(const FilterArgs& a, int metric, hipStream_t stream) {
+  const size_t smem = sizeof(Img8Shared);
+  const int nch = ((a.d + 31) / 32 + kT8CK - 1) / kT8CK;
+  const void* fn = nch <= 1   ? img8_fn<1>(metric)
+                   : nch == 2 ? img8_fn<2>(metric)
+                   : nch == 3 ? img8_fn<3>(metric)
+                   : nch == 4 ? img8_fn<4>(metric)
+                   : nch == 5 ? img8_fn<5>(metric)
+                              : img8_fn<6>(metric);
+  if (int rc = allow_lds(fn)) return rc;
+  int cus = 0;
+  int rc = device_cus(&cus);
+  if (rc) return rc;
+  const int64_t qtiles = (a.nq + fBQ - 1) / fBQ;
+  int64_t bx = (int64_t)cus;  // one workgroup per CU (its LDS)
+  if (bx > a.num_tiles * kT8Sub) bx = a.num_tiles * kT8Sub;
+  for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
+    FilterArgs b = a;
+    const int64_t yn = (qtiles - y0) < 65535 ? (qtiles - y0) : 65535;
+    b.Qh = a.Qh + y0 * fBQ * 32;
+    b.qinfo = a.qinfo + y0 * fBQ * kI8QInfo;
+    b.thr = a.thr + y0 * fBQ;
+    b.count = a.count + y0 * fBQ * kCountStride;
+    b.cand = a.cand + y0 * fBQ * (int64_t)a.cap;
+    if (a.cand_ub) b.cand_ub = a.cand_ub + y0 * fBQ * (int64_t)a.cap;
+    b.nq = a.nq - y0 * fBQ;
+    void* args[] = {(void*)&b};
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(kT8Threads), args,
+                                   smem, stream);
+    if (e != hipSuccess) {
+      set_error("filter_img8_kernel launch: %s", hipGetErrorString(e));
+      return FX_EHIP;
+    }
+  }
+  return check_launch("filter_img8_kernel");
+}
+#endif  // FX_FILTER_BQ >= 256
+
 #if FX_FILTER_BQ <= 128
 // ---- int8 image, a resident query slice (filter_img6_kernel)
 //
@@ -3450,6 +3865,9 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
 #elif FX_FILTER_IMG4
     return launch_img4(a, metric, stream);
 #elif FX_FILTER_IMG3
+#if FX_FILTER_BQ >= 256
+    if (img8_serves(a)) return launch_img8(a, metric, stream);
+#endif
     return launch_img3(a, metric, stream);
 #elif FX_FILTER_IMG2
     return launch_img2(a, metric, stream);
