@@ -1219,6 +1219,32 @@ __device__ __forceinline__ void i3_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// LDS appends through inline asm: the compiler cannot tell the append
+// segments from an LDS-DMA ring, so in a kernel with one it put vmcnt(0)
+// before a plain ds_add_rtn / ds_write -- waiting for the ring's chunks in
+// flight, about 1-2 us per wave and tile with an append (filter_img8_kernel:
+// configs[2]'s F2 ran 1.94 ms with its appends, 1.09 without them).  The
+// segments are never DMA targets; the flush reads them behind a barrier.
+__device__ __forceinline__ uint32_t lds_add_rtn_u32(uint32_t* p, uint32_t v) {
+  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(p);
+  uint32_t r;
+  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a), "v"(v) : "memory");
+  return r;
+}
+__device__ __forceinline__ void lds_write1_u32(uint32_t* p, uint32_t x) {
+  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(p);
+  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(x) : "memory");
+}
+__device__ __forceinline__ void lds_write2_u32(uint2* p, uint32_t x, uint32_t y) {
+  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint2*)(p);
+  asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(uint2{x, y}) : "memory");
+}
+__device__ __forceinline__ void lds_write3_u32(uint32_t* p, uint32_t x, uint32_t y, uint32_t z) {
+  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(p);
+  asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %0, %2 offset:4\n\tds_write_b32 %0, %3 offset:8"
+               ::"v"(a), "v"(x), "v"(y), "v"(z) : "memory");
+}
+
 // The pass test and appends of one wave's 32-row tile (RT = 1) against all
 // kI2QT query tiles; appends into LDS segments (filter_epilogue_seg's layout).
 template <int METRIC>
@@ -1269,7 +1295,7 @@ __device__ __forceinline__ void i3_epilogue(const f32x16 (&acc)[kI2QT], const fl
     const int qi = u * 32 + (int)opaque((unsigned)l32);  // (not hoisted: spilled)
     const int64_t gq = q0 + qi;
     uint32_t bits = pm[u];
-    uint32_t p = bits != 0u ? atomicAdd(&seg[qi], (uint32_t)__popc(bits)) : 0u;
+    uint32_t p = bits != 0u ? lds_add_rtn_u32(&seg[qi], (uint32_t)__popc(bits)) : 0u;
     const f32x4 qc = qtab[qi];
     const float qc1 = qc[0], qc0 = qc[1], qA = qc[2], qB = qc[3];
     const bool fq = !(qA <= 3.4e38f);
@@ -1319,10 +1345,7 @@ __device__ __forceinline__ void i3_epilogue(const f32x16 (&acc)[kI2QT], const fl
       }
       const uint32_t grow = (uint32_t)(a.row_base + r0) + (uint32_t)lr;
       if (p < (uint32_t)SEG) {
-        uint32_t* e = seg + fBQ + 3 * (qi * SEG + p);
-        e[0] = order_key(lb);
-        e[1] = order_key(ub);
-        e[2] = grow;
+        lds_write3_u32(seg + fBQ + 3 * (qi * SEG + p), order_key(lb), order_key(ub), grow);
       } else {  // rare: past the segment, global slots for the lane's remaining passes
         if (gp == ~0u) gp = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(rest));
         if (gp < (uint32_t)a.cap) {
@@ -1574,7 +1597,7 @@ __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const fl
     const int qi = u * 32 + (int)opaque((unsigned)l32);  // (not hoisted: spilled)
     const int64_t gq = q0 + qi;
     uint32_t bits = pm[u];
-    uint32_t p = bits != 0u ? atomicAdd(&seg[qi], (uint32_t)__popc(bits)) : 0u;
+    uint32_t p = bits != 0u ? lds_add_rtn_u32(&seg[qi], (uint32_t)__popc(bits)) : 0u;
     const f32x4 qrec = qinf[qi];
     uint32_t gp = ~0u;
     while (bits != 0u) {
@@ -1599,10 +1622,7 @@ __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const fl
       i8_bounds<METRIC>(x, rinfo[lr], rterm[lr], rext[lr], qrec, a.d, lb, ub);
       const uint32_t grow = rrow[lr];
       if (p < (uint32_t)SEG) {
-        uint32_t* e = seg + fBQ + 3 * (qi * SEG + p);
-        e[0] = order_key(lb);
-        e[1] = order_key(ub);
-        e[2] = grow;
+        lds_write3_u32(seg + fBQ + 3 * (qi * SEG + p), order_key(lb), order_key(ub), grow);
       } else {  // rare: past the segment, global slots for the lane's remaining passes
         if (gp == ~0u) gp = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(rest));
         if (gp < (uint32_t)a.cap) {
@@ -2040,7 +2060,7 @@ static int launch_img3(const FilterArgs& a, int metric, hipStream_t stream) {
 #define FX_T8_SLOTS 4  // ring slots of 16 KB (FX_T8_SLOTS - 1 chunks in flight)
 #endif
 #ifndef FX_T8_SEG
-#define FX_T8_SEG 24   // LDS append entries per query (overflow: global slots)
+#define FX_T8_SEG 40   // LDS append entries per query (8 B each; past them: global slots)
 #endif
 #ifndef FX_T8_PAIR
 #define FX_T8_PAIR 1   // 1: the ring refilled two chunks at a time, one barrier per two
@@ -2062,6 +2082,7 @@ constexpr int kT8Slots = FX_T8_SLOTS;
 constexpr int kT8QA = kT8Slots - 1;                   // chunks in flight
 constexpr int kT8Dma = kT8SlotBytes / 1024 / kT8Waves;  // 1-KB DMAs per wave per chunk
 constexpr int kT8SEG = FX_T8_SEG;
+constexpr int kT8Hi = kT8SEG * 3 / 4;  // a segment this full asks for a flush
 static_assert(kT8Waves * 32 == fBQ && kT8Sub * kT8BM == fBM && kT8Dma == 2 &&
                   kT8RT * kT8CK == kT8Waves * kT8Dma,
               "filter_img8_kernel tiling");
@@ -2074,17 +2095,20 @@ struct Img8Shared {
   uint32_t rkeep[kT8BM];  // 1: a row in range and not masked out
   f32x4 qtab[fBQ];
   f32x4 qinf[fBQ];
-  uint32_t seg[fBQ + 3 * fBQ * kT8SEG];
-  uint32_t segbase[fBQ];
+  uint32_t segc[fBQ];     // appends per query since the last flush (past kT8SEG: global)
+  uint32_t segn[fBQ];     // (flush) entries of the query's segment
+  uint32_t segbase[fBQ];  // (flush) their first candidate slot
+  uint32_t flush;         // a segment passed kT8Hi: flush at the next tile start
+  uint2 sege[fBQ * kT8SEG];  // entries {accumulator bits, image row}; bounds at the flush
 };
 static_assert(sizeof(Img8Shared) <= 160 * 1024, "filter_img8_kernel: LDS over 160 KB");
 
 // Pass test and appends of one wave's (32 queries x 128 rows) accumulators:
 // acc[t] element j is row 32 t + l32 against query 32 wid + (j & 3) + 8 (j >> 2) + 4 h.
 template <int METRIC>
-__device__ __forceinline__ void t8_epilogue(const f32x16 (&acc)[kT8RT], const Img8Shared* sh,
-                                            uint32_t* seg, const FilterArgs& a, int64_t q0,
-                                            int wid, int h, int l32) {
+__device__ __forceinline__ void t8_epilogue(const f32x16 (&acc)[kT8RT], Img8Shared* sh,
+                                            const FilterArgs& a, int64_t q0, int64_t r0, int wid,
+                                            int h, int l32) {
   constexpr int SEG = kT8SEG;
   float om[kT8RT], y1[kT8RT], y2[kT8RT];
   uint32_t keep[kT8RT];
@@ -2131,13 +2155,22 @@ __device__ __forceinline__ void t8_epilogue(const f32x16 (&acc)[kT8RT], const Im
     any |= pm[t];
   }
   if (__ballot(any != 0u) == 0ull) return;
+#ifdef FX_T8_DIAG  // 4: the pass test without its appends (the final pass only)
+  if ((FX_T8_DIAG & 4) && a.skip_full) {
+    if (any == 0x12345u) a.count[0] = 7;
+    return;
+  }
+#endif
+  // appends: the accumulator bits and the image row into the query's LDS
+  // segment (8 B; the bounds are computed at the flush, t8_flush); past the
+  // segment (rare: the flush keeps it under kT8Hi between tiles) a global
+  // slot with the bounds computed here
   static_for<kT8RT>([&](auto tc) {
     constexpr int t = decltype(tc)::value;
     uint32_t bits = pm[t];
     if (__ballot(bits != 0u) == 0ull) return;
     const int lr = t * 32 + (int)opaque((unsigned)l32);
-    const float ys = sh->rext[lr];
-    const uint32_t grow = sh->rrow[lr];
+    const uint32_t irow = (uint32_t)(r0 + lr);
     while (bits != 0u) {
       const int j = __builtin_ctz(bits);
       bits &= bits - 1u;
@@ -2155,16 +2188,28 @@ __device__ __forceinline__ void t8_epilogue(const f32x16 (&acc)[kT8RT], const Im
       for (int i = 0; i < 2; ++i) v2[i] = pick(v4[2 * i], v4[2 * i + 1], m2);
       const float x = pick(v2[0], v2[1], m3);
       const int qi = qb + (j & 3) + 8 * (j >> 2);
-      const int64_t gq = q0 + qi;
-      float lb, ub;
-      i8_bounds<METRIC>(x, om[t], y1[t], ys, sh->qinf[qi], a.d, lb, ub);
-      const uint32_t p = atomicAdd(&seg[qi], 1u);
+#ifdef FX_T8_DIAG  // (timing builds, the final pass only: 8 no LDS atomic, 16 no entry
+                   // write, 32 neither; its flush writes nothing)
+      uint32_t p;
+      if ((FX_T8_DIAG & 40) && a.skip_full)
+        p = (uint32_t)j & 15u;
+      else
+        p = lds_add_rtn_u32(&sh->segc[qi], 1u);
+      if ((FX_T8_DIAG & 48) && a.skip_full) {
+        if (__float_as_uint(x) == 0x12345u && p == 3u) a.count[0] = irow;
+        continue;
+      }
+#else
+      const uint32_t p = lds_add_rtn_u32(&sh->segc[qi], 1u);
+#endif
       if (p < (uint32_t)SEG) {
-        uint32_t* e = seg + fBQ + 3 * (qi * SEG + p);
-        e[0] = order_key(lb);
-        e[1] = order_key(ub);
-        e[2] = grow;
-      } else {  // rare: past the segment, a global slot
+        lds_write2_u32(&sh->sege[qi * SEG + p], __float_as_uint(x), irow);
+        if (p == (uint32_t)kT8Hi) lds_write1_u32(&sh->flush, 1u);
+      } else {
+        const int64_t gq = q0 + qi;
+        float lb, ub;
+        i8_bounds<METRIC>(x, om[t], y1[t], sh->rext[lr], sh->qinf[qi], a.d, lb, ub);
+        const uint32_t grow = sh->rrow[lr];
         const uint32_t gp = atomicAdd(&a.count[gq * kCountStride], 1u);
         if (gp < (uint32_t)a.cap) {
           const size_t slot = (size_t)gq * a.cap + gp;
@@ -2178,6 +2223,55 @@ __device__ __forceinline__ void t8_epilogue(const f32x16 (&acc)[kT8RT], const Im
       }
     }
   });
+}
+
+// Write the segments out (every thread; between two barriers of the tile
+// loop, or at the end): one global atomic per query reserves the slots, the
+// entries get their bounds from the row's terms (a.rowinfo) and the query's
+// record; RESET empties the segments for the next tiles.
+template <int METRIC, bool RESET>
+__device__ __forceinline__ void t8_flush(Img8Shared* sh, const FilterArgs& a, int64_t q0, int tid) {
+  constexpr int SEG = kT8SEG;
+#ifdef FX_T8_DIAG
+  if ((FX_T8_DIAG & 56) && a.skip_full) {  // (entries not written: nothing to flush)
+    __syncthreads();
+    for (int q = tid; q < fBQ; q += kT8Threads) sh->segc[q] = 0u;
+    if (tid == 0) sh->flush = 0u;
+    return;
+  }
+#endif
+  for (int q = tid; q < fBQ; q += kT8Threads) {
+    const uint32_t n = sh->segc[q] < (uint32_t)SEG ? sh->segc[q] : (uint32_t)SEG;
+    sh->segn[q] = n;
+    sh->segbase[q] = n != 0u && q0 + q < a.nq ? atomicAdd(&a.count[(q0 + q) * kCountStride], n) : 0u;
+  }
+  __syncthreads();
+  for (int i = tid; i < fBQ * SEG; i += kT8Threads) {
+    const int q = i / SEG, j = i % SEG;
+    if ((uint32_t)j >= sh->segn[q]) continue;
+    const uint32_t p = sh->segbase[q] + (uint32_t)j;
+    if (p >= (uint32_t)a.cap) continue;
+    const uint2 e = sh->sege[i];
+    const int64_t row = (int64_t)e.y;
+    const f32x4 ri = *reinterpret_cast<const f32x4*>(a.rowinfo + row * kI8RowInfo);
+    const float y1 = METRIC == 1 ? ri[1] : METRIC == 2 ? ri[2] : ri[3];
+    float lb, ub;
+    i8_bounds<METRIC>(__uint_as_float(e.x), ri[0], y1, ri[1], sh->qinf[q], a.d, lb, ub);
+    const uint32_t grow = (uint32_t)a.row_base + perm_row(a.perm_a, a.n, row);
+    const size_t slot = (size_t)(q0 + q) * a.cap + p;
+    if (a.cand_ub != nullptr) {
+      a.cand[slot] = make_comp(lb, grow);
+      a.cand_ub[slot] = make_comp(ub, grow);
+    } else {
+      a.cand[slot] = make_comp(ub, grow);
+    }
+  }
+  if constexpr (RESET) {
+    __syncthreads();  // (every entry read)
+    for (int q = tid; q < fBQ; q += kT8Threads) sh->segc[q] = 0u;
+    if (tid == 0) sh->flush = 0u;
+    // (the next appends follow the tile's epilogue barrier)
+  }
 }
 
 // NCH: ring chunks per tile, ceil(ceil(d / 32) / 4) (a compile-time chunk
@@ -2206,7 +2300,8 @@ __global__ void __launch_bounds__(kT8Threads, 2) filter_img8_kernel(FilterArgs a
     if (__syncthreads_and(full)) return;
   }
   i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, kT8Threads);
-  for (int q = tid; q < fBQ; q += kT8Threads) sh->seg[q] = 0u;
+  for (int q = tid; q < fBQ; q += kT8Threads) sh->segc[q] = 0u;
+  if (tid == 0) sh->flush = 0u;
   // the wave's 32 queries, every k-step: chunk c of query q is 64 B at
   // (c * qstride + q) * 64 (qprep8), k-step s its half s & 1 (zeros past dq)
   i32x4 qa[kT8KS];
@@ -2296,6 +2391,11 @@ __global__ void __launch_bounds__(kT8Threads, 2) filter_img8_kernel(FilterArgs a
         i3_wait_barrier<(kT8QA - 1) * kT8Dma>();
         issue();
       }
+      // (after the tile's first barrier every wave is past the last
+      // epilogue: a segment that passed kT8Hi is written out now)
+      if constexpr (C == 0) {
+        if (sh->flush) t8_flush<METRIC, true>(sh, a, q0, tid);
+      }
       if constexpr (C == 0) {  // the rows' terms and mask words of this tile
         const int64_t row = r0 + lr < a.n ? r0 + lr : a.n - 1;
         rsum = *reinterpret_cast<const f32x4*>(a.rowinfo + row * kI8RowInfo);
@@ -2322,6 +2422,13 @@ __global__ void __launch_bounds__(kT8Threads, 2) filter_img8_kernel(FilterArgs a
           constexpr int s = (C + j / kT8CK) * kT8CK + j % kT8CK;  // the query k-step
 #pragma unroll
           for (int t = 0; t < kT8RT; ++t) {
+#ifdef FX_T8_DIAG  // 2: no MFMA in the final pass (the B reads stay live)
+            if ((FX_T8_DIAG & 2) && a.skip_full) {
+              if (s == 0) acc[t] = acc0;
+              acc[t][0] += __builtin_bit_cast(float, b[t][0] ^ qa[s][0]);
+              continue;
+            }
+#endif
             const f32x16 cin = s == 0 ? acc0 : acc[t];
             acc[t] = __builtin_bit_cast(
                 f32x16, __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], b[t],
@@ -2373,12 +2480,19 @@ __global__ void __launch_bounds__(kT8Threads, 2) filter_img8_kernel(FilterArgs a
     // (the barrier also separates the tile's last MFMAs from the epilogue's
     // reads of their accumulators)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    t8_epilogue<METRIC>(acc, sh, sh->seg, a, q0, wid, h, l32);
+#ifdef FX_T8_DIAG  // (timing builds only: 1 no epilogue in the final pass)
+    if ((FX_T8_DIAG & 1) && a.skip_full) {
+      if (acc[0][0] == 1.2345f && acc[3][15] == 2.f) a.count[0] = 7;
+      continue;
+    }
+#endif
+    t8_epilogue<METRIC>(acc, sh, a, q0, r0, wid, h, l32);
   }
   // the ring's last DMAs (past the end) land before the workgroup's LDS is
   // released; then the segments go out
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  filter_flush_segments<kT8SEG, kT8Threads>(sh->seg, sh->segbase, a, q0, tid);
+  __syncthreads();
+  t8_flush<METRIC, false>(sh, a, q0, tid);
 }
 
 static bool img8_serves(const FilterArgs& a) {
