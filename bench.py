@@ -513,9 +513,14 @@ def main():
         # rows (the rescoring reads a few thousand rows per query on top)
         scan_bytes = img_bytes + nq * d * 4
     if filt:
-        kname = (f"fx::{'filter_img6_kernel' if bits == 8 and nq <= 128 else 'filter_img3_kernel'} "
-                 f"({'int8' if bits == 8 else 'fp16'}-MFMA bound filter, "
-                 "all sample phases) + exact rescoring of the candidates")
+        if bits == 8 and nq <= 128:
+            kname = "fx::filter_img6_kernel (int8-MFMA bound filter, all sample phases)"
+        elif bits == 8 and d <= 768:
+            kname = ("fx::filter_img8_kernel (int8-MFMA bound filter, queries in registers; "
+                     "filter_img3_kernel for the all-pass first sample)")
+        else:
+            kname = f"fx::filter_img3_kernel ({'int8' if bits == 8 else 'fp16'}-MFMA bound filter, all sample phases)"
+        kname += " + exact rescoring of the candidates"
     elif qu8:
         kname = "fx::scan_kernel<uint8> (quint8 codes dequantised in registers) + merge"
     else:

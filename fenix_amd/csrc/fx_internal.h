@@ -30,6 +30,7 @@ enum Option : int {
   kOptSingleImage,  // single queries over large f32 corpora through a supplied int8 image
   kOptI8MaxK,       // largest k an int8 filter image serves
   kOptImg6,         // int8 images: resident-query-slice kernel (1: <= 128 queries, 2: all, 0: off)
+  kOptImg8,         // int8 images: queries-in-registers kernel for > 128 queries, d <= 768 (0: off)
   kOptCount
 };
 int64_t option(Option o);

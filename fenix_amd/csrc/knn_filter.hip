@@ -2496,7 +2496,8 @@ __global__ void __launch_bounds__(kT8Threads, 2) filter_img8_kernel(FilterArgs a
 }
 
 static bool img8_serves(const FilterArgs& a) {
-  return FX_I8T && a.img8 && !a.all_pass && a.dq <= kT8KS * 32 && (a.d + 31) / 32 <= kT8KS;
+  return FX_I8T && a.img8 && !a.all_pass && a.dq <= kT8KS * 32 && (a.d + 31) / 32 <= kT8KS &&
+         option(kOptImg8) != 0;
 }
 
 template <int NCH>

@@ -95,6 +95,10 @@ int fx_device_count(int* out);
  *                            kernel; 2: larger batches too (as several
  *                            slices); 0: every batch the streamed-query-tile
  *                            kernel
+ *   "img8"                1  1: int8-image batches of > 128 queries with d <= 768
+ *                            run the queries-in-registers kernel (except the
+ *                            all-pass first sample); 0: the streamed-query-tile
+ *                            kernel
  *   "force_fallback"      0  1: every batched query is recomputed by the exact
  *                            single-query scan, as if its candidates overflowed
  *   "scan_interleave"    -1  -1: by row size; 0: one row range per workgroup;

@@ -845,6 +845,50 @@ def test_img6_resident_slices_equal_streamed_tile(eng, metric):
 
 
 @pytest.mark.parametrize("metric", METRICS)
+@pytest.mark.parametrize("d", [136, 768])
+def test_img8_queries_in_registers_equal_streamed_tile(eng, metric, d):
+    """Int8-image batches of more than 128 queries with d <= 768 run
+    filter_img8_kernel (option "img8": the queries as MFMA A operands in
+    registers, the image through an LDS-DMA ring, 8-byte append entries
+    bounded at the flush) for every phase but the all-pass first sample; the
+    same integer products, the same f32 pass test per (row, query) pair and
+    the same bounds as filter_img3_kernel, so the same candidate counts and
+    results bit for bit, equal to the exact scan -- over partial query tiles
+    (129, 300), a partial last ring chunk (d 136: 5 k-steps), rows the image
+    cannot represent and a mask."""
+    n, k = 60_000, 30
+    xh = _extreme_rows(n, d, 81)
+    x = torch.from_numpy(xh).to(eng.device)
+    eng.clear_images()
+    mask = np.random.RandomState(82).rand(n) < 0.8
+    m = _lib.METRICS[metric]
+    for nq in (129, 256, 300):
+        qh = O.fill_normal(nq, d, seed=83 + nq)
+        qh[3] = xh[17] * 2.0
+        q = torch.from_numpy(qh).to(eng.device)
+        for msk in (None, mask):
+            dm = device_mask(msk, eng.device) if msk is not None else None
+            got = {}
+            for img8 in (1, 0):
+                with _lib.options(img8=img8, filter_image=8):
+                    st = eng.scan(Shard(x, 0), q, m, k, dm)
+                    counts, cap = eng.filter_counts(Shard(x, 0), nq, m, k, st)
+                    od = torch.empty((nq, k), dtype=torch.float32, device=eng.device)
+                    orow = torch.empty((nq, k), dtype=torch.int64, device=eng.device)
+                    eng.reduce(Shard(x, 0), q, m, k, st, od, orow, dm)
+                    got[img8] = (counts, od.cpu().numpy(), orow.cpu().numpy())
+            assert got[1][0] is not None
+            np.testing.assert_array_equal(got[1][0], got[0][0], err_msg=f"nq {nq} mask {msk is not None}")
+            np.testing.assert_array_equal(got[1][2], got[0][2])
+            np.testing.assert_array_equal(got[1][1].view(np.uint32), got[0][1].view(np.uint32))
+            with _lib.options(batched=0):
+                sd, sr = gpu_search(eng, x, qh, metric, k, mask=msk)
+            np.testing.assert_array_equal(got[1][2], sr)
+            np.testing.assert_array_equal(got[1][1].view(np.uint32), sd.view(np.uint32))
+    eng.clear_images()
+
+
+@pytest.mark.parametrize("metric", METRICS)
 def test_small_batches_rescore_all_and_fallback_lists(eng, metric):
     """One or two queries through the int8 image skip the final exact
     threshold and rescore every candidate under F1's (rescore_dense_kernel);
@@ -882,12 +926,13 @@ def test_filter_candidate_counts_repeat_exactly(eng, img6):
     kernel without its pre-epilogue barrier moved in 201 of 232 repetitions,
     DESIGN.md 3.6d item 7).  nq 1-64 run the q64i build (img6 1 and 2: its
     resident-slice kernel, configs[1]'s product default for a single query),
-    65 the q128 build, 256 the 256-query tiles or two slices;
+    65 the q128 build, 256 and 300 the queries-in-registers kernel
+    (filter_img8_kernel) or two slices;
     batch_min_queries=1 sends the single query through the filter."""
     n, d, k = 70_000, 768, 30
     x = torch.from_numpy(_extreme_rows(n, d, 49)).to(eng.device)
     eng.clear_images()
-    for nq in (1, 2, 16, 64, 65, 256):
+    for nq in (1, 2, 16, 64, 65, 256, 300):
         q = torch.from_numpy(O.fill_normal(nq, d, seed=60 + nq)).to(eng.device)
         with _lib.options(img6=img6, filter_image=8, batch_min_queries=1):
             ref = None
