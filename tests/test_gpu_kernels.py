@@ -845,7 +845,7 @@ def test_img6_resident_slices_equal_streamed_tile(eng, metric):
 
 
 @pytest.mark.parametrize("metric", METRICS)
-@pytest.mark.parametrize("d", [136, 768])
+@pytest.mark.parametrize("d", [40, 136, 300, 768])
 def test_img8_queries_in_registers_equal_streamed_tile(eng, metric, d):
     """Int8-image batches of more than 128 queries with d <= 768 run
     filter_img8_kernel (option "img8": the queries as MFMA A operands in
@@ -854,8 +854,9 @@ def test_img8_queries_in_registers_equal_streamed_tile(eng, metric, d):
     same integer products, the same f32 pass test per (row, query) pair and
     the same bounds as filter_img3_kernel, so the same candidate counts and
     results bit for bit, equal to the exact scan -- over partial query tiles
-    (129, 300), a partial last ring chunk (d 136: 5 k-steps), rows the image
-    cannot represent and a mask."""
+    (129, 300), ring chunks per tile odd (d 40: 1, d 300: 3; one barrier per
+    chunk) and even (136: 2 with a partial last chunk, 768: 6; one per
+    pair), rows the image cannot represent and a mask."""
     n, k = 60_000, 30
     xh = _extreme_rows(n, d, 81)
     x = torch.from_numpy(xh).to(eng.device)
