@@ -2105,10 +2105,10 @@ static_assert(sizeof(Img8Shared) <= 160 * 1024, "filter_img8_kernel: LDS over 16
 
 // Pass test and appends of one wave's (32 queries x 128 rows) accumulators:
 // acc[t] element j is row 32 t + l32 against query 32 wid + (j & 3) + 8 (j >> 2) + 4 h.
-template <int METRIC>
+template <int METRIC, bool ALL>
 __device__ __forceinline__ void t8_epilogue(const f32x16 (&acc)[kT8RT], Img8Shared* sh,
-                                            const FilterArgs& a, int64_t q0, int64_t r0, int wid,
-                                            int h, int l32) {
+                                            const FilterArgs& a, int64_t q0, int64_t r0, int64_t ti,
+                                            int wid, int h, int l32) {
   constexpr int SEG = kT8SEG;
   float om[kT8RT], y1[kT8RT], y2[kT8RT];
   uint32_t keep[kT8RT];
@@ -2121,6 +2121,44 @@ __device__ __forceinline__ void t8_epilogue(const f32x16 (&acc)[kT8RT], Img8Shar
     keep[t] = sh->rkeep[lr] ? 0xffffu : 0u;
   }
   const int qb = wid * 32 + 4 * h;  // query of element j: qb + (j & 3) + 8 (j >> 2)
+  if constexpr (ALL) {
+    // a sampling phase's first launch (upper bounds only, then the k-th
+    // smallest): every pair, at a fixed slot -- tile ti's row lr at ti * 128
+    // + lr (the plan keeps the phase within cap), an empty key for a row
+    // that is masked out or past the end; the counts are set by workgroup 0
+    // (the element loop rolled, its accumulator picked by a select tree:
+    // 64 unrolled bounds spilled)
+    auto pick = [](float lo, float hi, uint32_t m) {
+      return __uint_as_float((__float_as_uint(hi) & m) | (__float_as_uint(lo) & ~m));
+    };
+#pragma unroll
+    for (int t = 0; t < kT8RT; ++t) {
+      const int lr = t * 32 + l32;
+      const uint32_t grow = sh->rrow[lr];
+      const float ys = sh->rext[lr];
+      const size_t p = (size_t)ti * kT8BM + lr;
+#pragma unroll 1
+      for (int j = 0; j < 16; ++j) {
+        const int qi = qb + (j & 3) + 8 * (j >> 2);
+        const int64_t gq = q0 + qi;
+        if (gq >= a.nq) continue;
+        const uint32_t m0 = 0u - ((uint32_t)j & 1u), m1 = 0u - (((uint32_t)j >> 1) & 1u);
+        const uint32_t m2 = 0u - (((uint32_t)j >> 2) & 1u), m3 = 0u - (((uint32_t)j >> 3) & 1u);
+        float v8[8], v4[4], v2[2];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v8[i] = pick(acc[t][2 * i], acc[t][2 * i + 1], m0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v4[i] = pick(v8[2 * i], v8[2 * i + 1], m1);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) v2[i] = pick(v4[2 * i], v4[2 * i + 1], m2);
+        float lb, ub;
+        i8_bounds<METRIC>(pick(v2[0], v2[1], m3), om[t], y1[t], ys, sh->qinf[qi], a.d, lb, ub);
+        __builtin_nontemporal_store(keep[t] ? make_comp(ub, grow) : kEmpty,
+                                    a.cand + (size_t)gq * a.cap + p);
+      }
+    }
+    return;
+  }
   uint32_t qlive = 0u;
 #pragma unroll
   for (int j = 0; j < 16; ++j)
@@ -2276,7 +2314,9 @@ __device__ __forceinline__ void t8_flush(Img8Shared* sh, const FilterArgs& a, in
 
 // NCH: ring chunks per tile, ceil(ceil(d / 32) / 4) (a compile-time chunk
 // loop: straight-line code, where the compiler counts every wait exactly)
-template <int METRIC, int NCH>
+// ALL: an all-pass sampling launch (t8_epilogue; its own instantiation, whose
+// unrolled bounds would otherwise spill the pass-test kernel's registers)
+template <int METRIC, int NCH, bool ALL>
 __global__ void __launch_bounds__(kT8Threads, 2) filter_img8_kernel(FilterArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   Img8Shared* sh = reinterpret_cast<Img8Shared*>(smem);
@@ -2301,6 +2341,9 @@ __global__ void __launch_bounds__(kT8Threads, 2) filter_img8_kernel(FilterArgs a
   }
   i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, kT8Threads);
   for (int q = tid; q < fBQ; q += kT8Threads) sh->segc[q] = 0u;
+  if (ALL && blockIdx.x == 0)  // every slot of the phase (t8_epilogue)
+    for (int q = tid; q < fBQ; q += kT8Threads)
+      if (q0 + q < a.nq) a.count[(q0 + q) * kCountStride] = (uint32_t)(ntiles * kT8BM);
   if (tid == 0) sh->flush = 0u;
   // the wave's 32 queries, every k-step: chunk c of query q is 64 B at
   // (c * qstride + q) * 64 (qprep8), k-step s its half s & 1 (zeros past dq)
@@ -2486,7 +2529,7 @@ __global__ void __launch_bounds__(kT8Threads, 2) filter_img8_kernel(FilterArgs a
       continue;
     }
 #endif
-    t8_epilogue<METRIC>(acc, sh, a, q0, r0, wid, h, l32);
+    t8_epilogue<METRIC, ALL>(acc, sh, a, q0, r0, ti, wid, h, l32);
   }
   // the ring's last DMAs (past the end) land before the workgroup's LDS is
   // released; then the segments go out
@@ -2496,26 +2539,35 @@ __global__ void __launch_bounds__(kT8Threads, 2) filter_img8_kernel(FilterArgs a
 }
 
 static bool img8_serves(const FilterArgs& a) {
-  return FX_I8T && a.img8 && !a.all_pass && a.dq <= kT8KS * 32 && (a.d + 31) / 32 <= kT8KS &&
-         option(kOptImg8) != 0;
+  // (an all-pass launch with both bounds -- a one-phase plan's F1 -- stays
+  // with the appending kernels; a sampling phase's slots fit: the plan keeps
+  // its rows within cap)
+  return FX_I8T && a.img8 && (!a.all_pass || (a.cand_ub == nullptr &&
+                                               a.num_tiles * fBM <= (int64_t)a.cap)) &&
+         a.dq <= kT8KS * 32 && (a.d + 31) / 32 <= kT8KS && option(kOptImg8) != 0;
 }
 
+template <int NCH, bool ALL>
+static const void* img8_fn_all(int metric) {
+  return metric == FX_METRIC_COS  ? (const void*)filter_img8_kernel<2, NCH, ALL>
+         : metric == FX_METRIC_IP ? (const void*)filter_img8_kernel<1, NCH, ALL>
+                                  : (const void*)filter_img8_kernel<0, NCH, ALL>;
+}
 template <int NCH>
-static const void* img8_fn(int metric) {
-  return metric == FX_METRIC_COS  ? (const void*)filter_img8_kernel<2, NCH>
-         : metric == FX_METRIC_IP ? (const void*)filter_img8_kernel<1, NCH>
-                                  : (const void*)filter_img8_kernel<0, NCH>;
+static const void* img8_fn(int metric, bool all) {
+  return all ? img8_fn_all<NCH, true>(metric) : img8_fn_all<NCH, false>(metric);
 }
 
 static int launch_img8(const FilterArgs& a, int metric, hipStream_t stream) {
   const size_t smem = sizeof(Img8Shared);
   const int nch = ((a.d + 31) / 32 + kT8CK - 1) / kT8CK;
-  const void* fn = nch <= 1   ? img8_fn<1>(metric)
-                   : nch == 2 ? img8_fn<2>(metric)
-                   : nch == 3 ? img8_fn<3>(metric)
-                   : nch == 4 ? img8_fn<4>(metric)
-                   : nch == 5 ? img8_fn<5>(metric)
-                              : img8_fn<6>(metric);
+  const bool all = a.all_pass != 0;
+  const void* fn = nch <= 1   ? img8_fn<1>(metric, all)
+                   : nch == 2 ? img8_fn<2>(metric, all)
+                   : nch == 3 ? img8_fn<3>(metric, all)
+                   : nch == 4 ? img8_fn<4>(metric, all)
+                   : nch == 5 ? img8_fn<5>(metric, all)
+                              : img8_fn<6>(metric, all);
   if (int rc = allow_lds(fn)) return rc;
   int cus = 0;
   int rc = device_cus(&cus);
