@@ -516,8 +516,7 @@ def main():
         if bits == 8 and nq <= 128:
             kname = "fx::filter_img6_kernel (int8-MFMA bound filter, all sample phases)"
         elif bits == 8 and d <= 768:
-            kname = ("fx::filter_img8_kernel (int8-MFMA bound filter, queries in registers; "
-                     "filter_img3_kernel for the all-pass first sample)")
+            kname = "fx::filter_img8_kernel (int8-MFMA bound filter, queries in registers, all phases)"
         else:
             kname = f"fx::filter_img3_kernel ({'int8' if bits == 8 else 'fp16'}-MFMA bound filter, all sample phases)"
         kname += " + exact rescoring of the candidates"
