@@ -7,6 +7,7 @@ bit-identically on the host for the oracle (oracle/knn_ref.c, float64).
 
 from __future__ import annotations
 
+import functools
 import json
 import os
 
@@ -612,6 +613,12 @@ def _extreme_rows(n, d, seed):
     return xh
 
 
+@functools.lru_cache(maxsize=4)
+def _extreme_rows_cached(n, d, seed):
+    """(one generation per shape across the metric parametrisations)"""
+    return _extreme_rows(n, d, seed)
+
+
 def _build_image(x, n, d):
     """fx_filter_image into buffers of fx_filter_image_bytes."""
     import ctypes
@@ -856,9 +863,12 @@ def test_img8_queries_in_registers_equal_streamed_tile(eng, metric, d):
     results bit for bit, equal to the exact scan -- over partial query tiles
     (129, 300), ring chunks per tile odd (d 40: 1, d 300: 3; one barrier per
     chunk) and even (136: 2 with a partial last chunk, 768: 6; one per
-    pair), rows the image cannot represent and a mask."""
-    n, k = 60_000, 30
-    xh = _extreme_rows(n, d, 81)
+    pair), rows the image cannot represent and a mask.  600 000 rows make a
+    three-phase plan (19, 293, 2 344 tiles): the all-pass first sample, F1
+    and F2 all run the kernel (a one- or two-phase plan's all-pass F1 keeps
+    both bounds and stays with the appending kernels)."""
+    n, k = 600_000, 30
+    xh = _extreme_rows_cached(n, d, 81)
     x = torch.from_numpy(xh).to(eng.device)
     eng.clear_images()
     mask = np.random.RandomState(82).rand(n) < 0.8

@@ -23,6 +23,8 @@ p.add_argument("--reps", type=int, default=30)
 p.add_argument("--nq", default="1,2,16,64,65,256", help="batch sizes (1-64: the q64i build)")
 p.add_argument("--img6", default="0,1,2", help="option img6 values")
 p.add_argument("--d", default="136,768")
+p.add_argument("--n", type=int, default=70_000,
+               help="rows (600000 and up: a 3-phase plan, every int8 phase in the batched kernels)")
 p.add_argument("--fp16", action="store_true",
                help="the fp16 filter kernels instead: fp16 image (k = 30) and no image (k = 300)")
 a = p.parse_args()
@@ -52,7 +54,7 @@ if a.fp16:
                           + ("no filter" if ref is None else
                              f"{moved} of {a.reps - 1} repetitions moved"), flush=True)
     sys.exit(0)
-for n, d in [(70_000, int(v)) for v in a.d.split(",")]:
+for n, d in [(a.n, int(v)) for v in a.d.split(",")]:
     xh = _extreme_rows(n, d, 49)
     x = torch.from_numpy(xh).to(eng.device)
     eng.clear_images()
