@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import warnings
 import weakref
 from collections import OrderedDict
 from dataclasses import dataclass, field
@@ -915,6 +916,18 @@ def search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: i
 
 # how many multi-device searches gathered their lists each way (bench.py, tests)
 GATHERS: Dict[str, int] = {"rccl": 0, "p2p": 0}
+_GATHERS_LOCK = threading.Lock()
+
+# Every grouped RCCL exchange of this process is enqueued under this one lock
+# (DESIGN §4).  Flight handlers run on concurrent gRPC threads
+# (reference: src/fenix/flight.py:62-77), and an fx_allgather_topk enqueues one
+# collective per device (ncclGroupStart … ncclAllGather × ndev … ncclGroupEnd,
+# comm.hip).  Two such enqueues that interleave can order collectives A, B on
+# device 0 and B, A on device 1; each RCCL kernel waits for its peers, so both
+# hang.  One lock for the whole process (not one per communicator) also orders
+# exchanges of communicators over overlapping device sets, which share the
+# devices' streams.
+COLLECTIVE_LOCK = threading.Lock()
 
 
 def gather_mode(devs: Sequence[torch.device]) -> str:
@@ -961,9 +974,13 @@ def _search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: 
         return per[0]
     devs = list(groups)
     if gather_mode(devs) == "rccl":
-        GATHERS["rccl"] += 1
-        return DeviceComm.get(devs).gather_merge(per, k)
-    GATHERS["p2p"] += 1
+        comm = DeviceComm.get_or_none(devs)
+        if comm is not None:
+            with _GATHERS_LOCK:
+                GATHERS["rccl"] += 1
+            return comm.gather_merge(per, k)
+    with _GATHERS_LOCK:
+        GATHERS["p2p"] += 1
     dev0 = next(iter(groups))
     with torch.cuda.device(dev0):
         eng0 = Engine.get(dev0)
@@ -978,9 +995,16 @@ class DeviceComm:
 
     ``gather_merge`` all-gathers every device's [nq, k] top-k with one grouped
     fx_allgather_topk and merges on the first device.  ``_search_all`` uses
-    it for distinct devices unless FENIX_AMD_GATHER=p2p (``gather_mode``)."""
+    it for distinct devices unless FENIX_AMD_GATHER=p2p (``gather_mode``).
+
+    The collective is enqueued under ``COLLECTIVE_LOCK``, so concurrent
+    searches reach every device's stream in one order.  A device set whose
+    communicator cannot be created (no RCCL, ncclCommInitAll failing) is
+    remembered, and ``get_or_none`` returns None for it, so ``_search_all``
+    takes the peer-copy path instead of failing every search."""
 
     _cache: Dict[tuple, "DeviceComm"] = {}
+    _failed: Dict[tuple, str] = {}
     _clock = threading.Lock()
 
     def __init__(self, devs: Sequence[torch.device]) -> None:
@@ -999,6 +1023,24 @@ class DeviceComm:
                 c = cls(devs)
                 cls._cache[key] = c
             return c
+
+    @classmethod
+    def get_or_none(cls, devs: Sequence[torch.device]) -> Optional["DeviceComm"]:
+        """``get``, or None (with one warning per device set) when the
+        communicator cannot be created."""
+        key = tuple(d.index for d in devs)
+        if key in cls._failed:
+            return None
+        try:
+            return cls.get(devs)
+        except (RuntimeError, OSError) as e:
+            with cls._clock:
+                first = key not in cls._failed
+                cls._failed[key] = str(e)
+            if first:
+                warnings.warn(f"RCCL communicator over devices {key} unavailable ({e}); "
+                              "gathering top-k lists by peer copies", RuntimeWarning)
+            return None
 
     def close(self) -> None:
         if self.handle:
@@ -1021,8 +1063,9 @@ class DeviceComm:
         dst_d = P(*[d.data_ptr() for d, _ in outs])
         dst_r = P(*[r.data_ptr() for _, r in outs])
         streams = P(*[torch.cuda.current_stream(dv).cuda_stream for dv in self.devs])
-        _lib.check(_lib.load().fx_allgather_topk(self.handle, src_d, src_r, nq, k, dst_d, dst_r,
-                                                 streams))
+        with COLLECTIVE_LOCK:
+            _lib.check(_lib.load().fx_allgather_topk(self.handle, src_d, src_r, nq, k,
+                                                     dst_d, dst_r, streams))
         return outs
 
     def gather_merge(self, per, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
