@@ -540,11 +540,14 @@ def main():
     if filt:  # the GEMM the filter evaluates, against the dense MFMA peak of its type
         roof["bytes_basis"] = "filter image + row terms (the pass reads these, not the rows)"
         roof["algorithmic_bytes"] = algo_bytes
-        roof["mfma_tflops"] = 2.0 * n * nq * d / (scan_ms * 1e-3) / 1e12
-        roof["mfma_peak_tflops"] = MFMA_F16_PEAK_TFS * (2 if bits == 8 else 1)
+        # int8 MFMA work is integer ops (TOPS), fp16 work flops (TFLOPS)
+        u = "tops" if bits == 8 else "tflops"
+        roof[f"mfma_{u}"] = 2.0 * n * nq * d / (scan_ms * 1e-3) / 1e12
+        roof[f"mfma_peak_{u}"] = MFMA_F16_PEAK_TFS * (2 if bits == 8 else 1)
     roof["frac"] = check_frac("roofline.frac", roof["achieved"] / roof["peak"])
-    if "mfma_tflops" in roof:
-        check_frac("roofline.mfma", roof["mfma_tflops"] / roof["mfma_peak_tflops"])
+    for u in ("tops", "tflops"):
+        if f"mfma_{u}" in roof:
+            check_frac("roofline.mfma", roof[f"mfma_{u}"] / roof[f"mfma_peak_{u}"])
 
     # the single-process path a Flight server runs over every GPU of the node
     # (engine._search_all): rank 0 alone, while the other ranks wait on the
@@ -570,9 +573,22 @@ def main():
     elif serve_devs is not None:
         serve = serve_leg(eng, serve_devs, n, d, k, metric, q, args, None)
 
+    # the CPU baseline is timed after every timed region, on rank 0 only; for
+    # N > 1 the other ranks wait on the rendezvous store (not a GPU barrier,
+    # so no collective kernel of theirs spins meanwhile)
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args)
+        finally:
+            if world > 1:
+                dist.distributed_c10d._get_default_store().set("fx_bench_cpu_done", "1")
+    elif world > 1 and not args.no_cpu_baseline:
+        dist.distributed_c10d._get_default_store().wait(["fx_bench_cpu_done"],
+                                                         datetime.timedelta(minutes=20))
+
     out = None
     if rank == 0:
-        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
         wl = (f"{n // 1_000_000 if n % 1_000_000 == 0 else n}"
               f"{'M' if n % 1_000_000 == 0 else ''}x{d} {args.dtype} {args.metric.upper()} "
               f"kNN k={k}, {'single query' if nq == 1 else f'{nq}-query batch'}, per GPU"
@@ -769,8 +785,8 @@ def batch_leg(eng, shard, image, img_bytes, n, d, k, args, nb=256, mname="cosine
         "achieved_gbs_over_image": pass_bytes / (span * 1e-3) / 1e9,
         "frac_over_image": check_frac("configs2.frac_over_image",
                                       pass_bytes / (span * 1e-3) / 1e9 / HBM_PEAK_GBS),
-        "mfma_tflops": 2.0 * n * nb * d / (span * 1e-3) / 1e12,
-        "mfma_peak_tflops": MFMA_F16_PEAK_TFS * 2,
+        "mfma_tops": 2.0 * n * nb * d / (span * 1e-3) / 1e12,   # int8 ops, not flops
+        "mfma_peak_tops": MFMA_F16_PEAK_TFS * 2,
         "traffic": traffic,
         "traffic_over_image": (traffic / pass_bytes) if traffic else None,
         "sample_bit_identical": same,

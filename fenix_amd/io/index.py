@@ -151,7 +151,8 @@ def _gather_vectors(shards, rows: np.ndarray, type: pa.DataType,
     into one result buffer on the first shard's device (other devices' rows
     travel there peer to peer), and ONE D2H into pinned memory with one
     synchronisation — not a round trip per shard (configs[4]'s 8 shards:
-    0.63 ms -> see profiles/r05_cfg4_serving_profile.md).  ``null``: which
+    0.63 -> 0.41 ms, profiles/r05_profile_call_cfg4_{before,after}.json,
+    DESIGN §6.2).  ``null``: which
     result rows are null slots of the column; their stored values are
     gathered like any other (they were scanned) and the slot stays null, as
     index.py:166's ``take`` keeps validity (tests/golden g7_nulls)."""
@@ -162,7 +163,12 @@ def _gather_vectors(shards, rows: np.ndarray, type: pa.DataType,
         out = np.empty((m, d), dtype=ndt)
     else:
         bases = np.array([s.row_base for s in shards], dtype=np.int64)
-        which = np.searchsorted(bases, rows, side="right") - 1  # shards are in row order
+        sizes_n = np.array([s.n for s in shards], dtype=np.int64)
+        if np.any(np.diff(bases) < 0):
+            raise ValueError("_gather_vectors: shards must be in row order")
+        which = np.searchsorted(bases, rows, side="right") - 1
+        if np.any(which < 0) or np.any(rows - bases[np.maximum(which, 0)] >= sizes_n[which]):
+            raise ValueError("_gather_vectors: a result row lies outside every shard")
         dev0 = shards[0].data.device
         with torch.cuda.device(dev0):
             acc = torch.empty((m, d), dtype=shards[0].data.dtype, device=dev0)

@@ -427,8 +427,9 @@ typedef struct fx_corpus {
  * smallest (distance, global row) over all of them.  The per-shard form
  * (fx_knn_search per shard + fx_topk_merge) runs a merge tree per shard and
  * one more over the shards.  Replaces index.py:162-168 over concatenated
- * sources.  Shards: same d, dtype FX_DTYPE_F32 or FX_DTYPE_F16, n >= 1,
- * each with its own row_base; masks: NULL, or one bitmap (or NULL) per
+ * sources.  Shards: same d, one dtype of FX_DTYPE_F32 / F16 / QU8 (each
+ * QU8 shard with its own scale and zero point), n >= 1, each with its own
+ * row_base; masks: NULL, or one bitmap (or NULL) per
  * shard.  k <= fx_max_k().  Exact scan only (a caller with a filter image
  * keeps the per-shard calls).  Results equal the per-shard form bit for bit.
  */

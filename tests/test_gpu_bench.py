@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import json
 import os
+import socket
 import subprocess
 import sys
 
@@ -17,6 +18,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
         "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
         "roofline", "cpu_baseline"}
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def run_bench(*args: str, env=None) -> dict:
@@ -59,7 +66,8 @@ def test_bench_rccl_path_one_rank():
     the 8-GPU scaling run makes."""
     env = dict(os.environ, FENIX_AMD_BENCH_DIST="1", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-           "--master-addr", "127.0.0.1", "--master-port", "29531", os.path.join(ROOT, "bench.py"),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "bench.py"),
            "--gpus", "1", "--rows", "300000", "--steps", "3", "--warmup", "1",
            "--no-cpu-baseline"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
@@ -78,11 +86,13 @@ def test_bench_gpus_n_launches_n_ranks():
     leg (--rows in total, half per rank) and the single-process serve leg
     (rank 0 alone, two shards through engine._search_all, merged on the one
     device since the ordinal repeats), whose result bench.py checks against
-    the ranks' merge."""
+    the ranks' merge.  rank 0 also times the CPU baseline after the timed
+    legs while rank 1 waits on the store, so the N > 1 line carries one."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     rec = run_bench("--gpus", "2", "--dist-backend", "gloo", "--rows", "200000", "--steps", "3",
-                    "--warmup", "1", "--no-cpu-baseline", "--serve-devices", "0,0", env=env)
+                    "--warmup", "1", "--cpu-rows", "20000", "--cpu-seconds", "0.5",
+                    "--serve-devices", "0,0", env=env)
     assert rec["n_gpus"] == 2
     assert rec["config"]["total_rows"] == 400000
     assert rec["config"]["parallelism"].startswith(
@@ -94,6 +104,8 @@ def test_bench_gpus_n_launches_n_ranks():
     assert "error" not in serve, serve
     assert list(serve["gathers"]) == ["none"]
     assert serve["gathers"]["none"]["equals_rank_path"] is True
+    cpu = rec["cpu_baseline"]
+    assert cpu is not None and cpu["kind"] == "port" and cpu["value"] > 0 and cpu["cores"] >= 1
 
 
 def test_bench_serve_devices_one_rank():

@@ -1151,18 +1151,28 @@ def test_interleaved_scan_equals_contiguous(eng, n, d, dtype, metric):
 
 
 @pytest.mark.parametrize("metric", METRICS)
-@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.uint8])
 def test_search_shards_one_merge_equals_per_shard(eng, metric, dtype):
     """fx_knn_search_shards (every shard's scan into one list buffer, ONE
     merge tree) returns the per-shard form's bits (a merge per shard, then
     fx_topk_merge over the shards), and the oracle's rows: shards of uneven
     sizes, one smaller than k, one 4 bytes off 16-byte alignment (the
     scalar-load scan), row bases with gaps (global rows of the sources as
-    numbered by table.py:19-21), k from 10 to the fused scan's 1 024."""
+    numbered by table.py:19-21), k from 10 to the fused scan's 1 024.
+    uint8: quint8 code shards (FX_DTYPE_QU8), each with its own
+    scale and zero point, all 16-B aligned; the oracle scans the dequantised
+    values (quint8.py:53-54)."""
     d = 136
     sizes = [50_000, 777, 20_000, 3_001]
     xs, shards, base = [], [], 0
-    for i, n in enumerate(sizes):
+    if dtype == torch.uint8:
+        for i, n in enumerate(sizes):
+            codes = np.random.RandomState(80 + i).randint(0, 128, size=(n, d)).astype(np.uint8)
+            scale, zp = float(np.float32(0.03 + 0.01 * i)), 60 + i
+            xs.append(O.dequantize(codes, scale, zp).astype(np.float32))
+            shards.append(Shard(torch.from_numpy(codes).to(eng.device), base, scale, zp))
+            base += n + 1000 * (i + 1)
+    for i, n in enumerate(sizes if dtype != torch.uint8 else []):
         x = gpu_fill(eng, n + (1 if i == 2 else 0), d, seed=80 + i, dtype=dtype)
         if i == 2:  # a view 1 row + 4 bytes in: not 16-B aligned
             flat = x.view(-1)[1 : 1 + n * d] if dtype == torch.float32 else x.view(-1)[2 : 2 + n * d]

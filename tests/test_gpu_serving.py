@@ -11,7 +11,7 @@ The latency is timed the way a client sees it: a torch-free client process
 (tools/bench_flight.py --client) over loopback gRPC, 20 warm searches, with a
 bound on the median.  The checks above run in this process, which also hosts
 the server; a search timed from here measured 28-29 ms in round 4 against
-5.3 ms from a separate client (profiles/r05_cfg4_serving_profile.md): the
+5.3 ms from a separate client (profiles/r05_cfg4_serving_test.json): the
 in-process client shares the server's interpreter and GIL, and this process
 imports torch, which a client never does."""
 
@@ -36,9 +36,15 @@ pytestmark = pytest.mark.gpu
 
 SHARDS, PER_SHARD, D, K = 8, 500_000, 1536, 1000
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# median of 20 warm searches from a separate client process (measured 5.3 ms
-# before the one-sync vector gather, profiles/r05_cfg4_serving_profile.md)
+# median of 20 warm searches from a separate client process (5.3 ms before the
+# one-sync vector gather, profiles/r05_cfg4_serving_test.json; 3.74 ms after,
+# profiles/r05_cfg4_serving_test2.json)
 MEDIAN_MS_BOUND = 6.0
+# positions (of 3 queries x 1 000) whose id differs from the float64 oracle at
+# a near-tie (tests/parity.py's rule): float32 accumulation cannot order rows
+# whose 1536-d fp16 inner products differ by < 2e-6 relative.  Measured: 2
+# (profiles/r05_cfg4_serving_test2.json).
+NEAR_TIE_CAP = 6
 VECTOR = pa.list_(pa.float16(), D)
 SCHEMA = pa.schema({"id": pa.int64(), "vector": VECTOR})
 
@@ -127,6 +133,7 @@ def test_configs4_flight_8_shards_f16_ip_k1000(tmp_path, monkeypatch):
                        "client_process_lat_ms": client["lat_ms"],
                        "client_process_median_ms": median_ms,
                        "inprocess_flight_search_s": times, "near_ties": near_ties}, f)
+        assert near_ties <= NEAR_TIE_CAP, near_ties
         assert median_ms <= MEDIAN_MS_BOUND, (median_ms, client["lat_ms"])
     finally:
         server.shutdown()

@@ -152,9 +152,13 @@ def test_configs4_50M_x1536_f16_ip_k1000_sharded_x8(eng):
 N3, D3, K3, G3 = 80_000_000, 768, 100, 8
 
 
-def _split_search(eng, cuts, q, planted, metric):
+def _split_search(eng, cuts, q, planted, metric, exact=False):
     """Regenerate each row range [a, b) of the 80M-row corpus into one buffer
-    (row_base = a), plant the rows it holds, search it; merge the lists."""
+    (row_base = a), plant the rows it holds, search it; merge the lists.
+    ``exact``: one query per call with the exact fused scan
+    (single_query_image=0), which is what every rank of the driver's N = 8
+    bench line runs on its 10M rows (bench.py); otherwise the product
+    default for the two-query batch (the int8 filter image)."""
     qt = torch.from_numpy(q)
     width = max(b - a for a, b in zip(cuts[:-1], cuts[1:]))
     buf = torch.empty((width, D3), dtype=torch.float32, device=eng.device)
@@ -167,9 +171,17 @@ def _split_search(eng, cuts, q, planted, metric):
         for r, v in planted.items():
             if a <= r < b:
                 x[r - a] = torch.from_numpy(v).to(eng.device)
-        d, r = eng.search([Shard(x, a)], qt, metric, K3)
-        pd[:, i] = d
-        pr[:, i] = r
+        if exact:
+            with _lib.options(single_query_image=0):
+                assert not _lib.filter_image_used(b - a, D3, _lib.DTYPE_F32, 1, K3, metric)
+                for j in range(nq):
+                    d, r = eng.search([Shard(x, a)], qt[j:j + 1], metric, K3)
+                    pd[j, i] = d[0]
+                    pr[j, i] = r[0]
+        else:
+            d, r = eng.search([Shard(x, a)], qt, metric, K3)
+            pd[:, i] = d
+            pr[:, i] = r
     torch.cuda.synchronize()
     del buf
     torch.cuda.empty_cache()
@@ -186,12 +198,22 @@ def test_configs3_80M_x768_f32_l2_k100_row_shards(eng):
     d3, r3 = _split_search(eng, three, q, planted, l2)
     assert torch.equal(r8, r3)
     assert torch.equal(d8.view(torch.int32), d3.view(torch.int32))
+    # the driver's N = 8 path: each 10M shard through the exact fused scan
+    e8d, e8r = _split_search(eng, eight, q, planted, l2, exact=True)
+    assert torch.equal(e8r, r8)
+    assert torch.equal(e8d.view(torch.int32), d8.view(torch.int32))
     r8h = r8.cpu().numpy()
     assert r8h[0, 0] == 71_234_567 and r8h[1, 0] == N3 - 1
     od, orow = O.knn_gen(N3, D3, 0, q, "l2", K3, overrides=planted)
     details = []
     near = check_topk(d8.cpu().numpy(), r8h, od, orow, O.fill_normal(100_000, D3, 0), q, "l2",
                       details=details)
-    record("configs[3]", {"near_ties": near, "positions": details})
-    print("configs[3] near-ties", near)
+    details_exact = []
+    near_exact = check_topk(e8d.cpu().numpy(), e8r.cpu().numpy(), od, orow,
+                            O.fill_normal(100_000, D3, 0), q, "l2", details=details_exact)
+    record("configs[3]", {"near_ties": near, "positions": details,
+                          "exact_scan_per_shard": {"near_ties": near_exact,
+                                                   "positions": details_exact}})
+    print("configs[3] near-ties", near, "exact", near_exact)
     assert near == 0, details  # bit-exact ids (measured: 0 near-ties)
+    assert near_exact == 0, details_exact
