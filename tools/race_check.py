@@ -23,6 +23,8 @@ p.add_argument("--reps", type=int, default=30)
 p.add_argument("--nq", default="1,2,16,64,65,256", help="batch sizes (1-64: the q64i build)")
 p.add_argument("--img6", default="0,1,2", help="option img6 values")
 p.add_argument("--d", default="136,768")
+p.add_argument("--img8", default="1", help="option img8 values (2: filter_img9_kernel)")
+p.add_argument("--metric", type=int, default=0, help="0 L2, 1 inner product, 2 cosine")
 p.add_argument("--n", type=int, default=70_000,
                help="rows (600000 and up: a 3-phase plan, every int8 phase in the batched kernels)")
 p.add_argument("--fp16", action="store_true",
@@ -62,20 +64,28 @@ for n, d in [(a.n, int(v)) for v in a.d.split(",")]:
     for nq in [int(v) for v in a.nq.split(",")]:
         q = torch.from_numpy(O.fill_normal(nq, d, seed=60 + nq)).to(eng.device)
         for msk in (None, mask):
-            for img6 in [int(v) for v in a.img6.split(",")]:
-                with _lib.options(img6=img6, filter_image=8, batch_min_queries=1):
+            first = None
+            for img6, img8 in [(int(v), int(w)) for v in a.img6.split(",") for w in a.img8.split(",")]:
+                with _lib.options(img6=img6, img8=img8, filter_image=8, batch_min_queries=1):
                     ref = None
                     moved = 0
                     for _ in range(a.reps):
-                        st = eng.scan(Shard(x, 0), q, 0, k, msk)
-                        c, _cap = eng.filter_counts(Shard(x, 0), nq, 0, k, st)
+                        st = eng.scan(Shard(x, 0), q, a.metric, k, msk)
+                        c, _cap = eng.filter_counts(Shard(x, 0), nq, a.metric, k, st)
                         if ref is None:
                             ref = c
                         elif not np.array_equal(c, ref):
                             moved += 1
                             diff = np.nonzero(c != ref)[0]
-                            print(f"   d {d} nq {nq} mask {msk is not None} img6 {img6}: queries "
-                                  f"{diff[:20].tolist()} {(c[diff] - ref[diff])[:20].tolist()}",
+                            print(f"   d {d} nq {nq} mask {msk is not None} img6 {img6} img8 {img8}: "
+                                  f"queries {diff[:20].tolist()} {(c[diff] - ref[diff])[:20].tolist()}",
                                   flush=True)
-                    print(f"d {d} nq {nq} mask {msk is not None} img6 {img6}: {moved} of "
-                          f"{a.reps - 1} repetitions moved", flush=True)
+                    same = None
+                    if first is None:
+                        first = ref
+                    else:
+                        same = bool(np.array_equal(ref, first))
+                    print(f"d {d} nq {nq} mask {msk is not None} img6 {img6} img8 {img8}: {moved} of "
+                          f"{a.reps - 1} repetitions moved"
+                          + ("" if same is None else f"; counts equal the first variant's: {same}"),
+                          flush=True)
