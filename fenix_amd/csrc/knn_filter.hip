@@ -2595,507 +2595,6 @@ static int launch_img8(const FilterArgs& a, int metric, hipStream_t stream) {
   }
   return check_launch("filter_img8_kernel");
 }
-
-// ---- int8 image, queries in registers, the pass test under the next tile's
-// MFMAs (filter_img9_kernel, option "img8" 2)
-//
-// filter_img8_kernel runs each 128-row tile's pass test and appends after a
-// barrier, while every wave of the workgroup is in its epilogue, so the matrix
-// pipe idles through them (0.24 + 0.18 ms of configs[2]'s
-// 1.85 ms final pass).  Here a workgroup tile is 64 rows (2 32-row MFMA tiles,
-// 32 accumulator registers) and the accumulators are double-buffered: tile i's
-// k-loop writes acc[i & 1] while, between its MFMAs, the wave runs tile i-1's
-// pass test on acc[(i - 1) & 1] one (query pair, row tile) unit per k-step,
-// then tile i-1's appends.  Same registers as img8 (2 x 2 x 16 accumulators;
-// half the B fragments).  The pass test is img8's, as scalar v_fma_f32 (packed
-// f32 VALU beside MFMAs costs issue cycles, MI355X_MICROARCH.md constants
-// table): the same f32 operations per (row, query) pair, the same decisions.
-// The accumulators a unit reads were last written by the previous tile's
-// MFMAs, behind that tile's last barrier and >= 4 MFMAs of this tile earlier
-// (DESIGN.md 3.6e).  Ring: 8 KB chunks (64 rows x 4 k-steps), one 1-KB DMA per
-// wave per chunk, 8 slots, one barrier per two chunks.  Not all-pass launches
-// (img8 keeps them).
-#ifndef FX_T9_EPI
-#define FX_T9_EPI 0  // diagnostic builds: 1 runs tile i-1's epilogue at tile i's start,
-                     // between two barriers (no MFMA of any wave beside it); 2 none at
-                     // all (timing only: no candidates)
-#endif
-constexpr int kT9BM = 64;                             // rows per workgroup tile
-constexpr int kT9RT = kT9BM / 32;                     // 32-row MFMA tiles
-constexpr int kT9Sub = fBM / kT9BM;                   // workgroup tiles per plan tile
-constexpr int kT9SlotBytes = kT9RT * kT8CK * 1024;    // 8 KB
-constexpr int kT9Slots = 8;
-constexpr int kT9Dma = kT9SlotBytes / 1024 / kT8Waves;  // 1
-static_assert(kT9Dma == 1 && kT9Sub * kT9BM == fBM && kT9Slots % 2 == 0, "filter_img9_kernel tiling");
-struct Img9Shared {
-  unsigned char ring[kT9Slots][kT9SlotBytes];
-  float rinfo[2][kT9BM];   // by tile parity: omega (NaN: forced)
-  float rterm[2][kT9BM];   // y1
-  float rext[2][kT9BM];    // 1 / s
-  uint32_t rrow[2][kT9BM];   // the global corpus row (image8_perm)
-  uint32_t rkeep[2][kT9BM];  // 0xffff: a row in range and not masked out
-  f32x4 qtab[fBQ];
-  f32x4 qinf[fBQ];
-  uint32_t segc[fBQ];
-  uint32_t segn[fBQ];
-  uint32_t segbase[fBQ];
-  uint32_t flush;
-  uint2 sege[fBQ * kT8SEG];
-};
-static_assert(sizeof(Img9Shared) <= 160 * 1024, "filter_img9_kernel: LDS over 160 KB");
-
-// tile i-1's epilogue state, carried through tile i's k-loop
-struct T9Epi {
-  float om[kT9RT], y1[kT9RT], y2[kT9RT];
-  uint32_t fail[kT9RT];
-  f32x4 ca, cb;  // the next pair group's query table entries
-};
-
-// the row terms of parity slot P into registers; fail bits cleared
-template <int METRIC>
-__device__ __forceinline__ void t9_epi_begin(T9Epi& e, const Img9Shared* sh, int P, int l32) {
-#pragma unroll
-  for (int t = 0; t < kT9RT; ++t) {
-    const int lr = t * 32 + l32;
-    e.om[t] = sh->rinfo[P][lr];
-    e.y1[t] = sh->rterm[P][lr];
-    e.y2[t] = METRIC == 0 ? sh->rext[P][lr] : 0.f;
-    e.fail[t] = 0u;
-  }
-}
-
-// Query pair group g of the pass test (g = 0 .. 7: pair jp = 7 - g, as
-// img8's pairs run down): t9_epi_load reads the two queries' table entries,
-// t9_epi_group runs the pair on both row tiles; the failing bits enter
-// last-in at bit 0 (element j + 1 first, then j)
-template <int G>
-__device__ __forceinline__ void t9_epi_load(T9Epi& e, const Img9Shared* sh, int qb) {
-  constexpr int j = 2 * (7 - G);
-  const int q = qb + (j & 3) + 8 * (j >> 2);
-  e.ca = sh->qtab[q];
-  e.cb = sh->qtab[q + 1];
-}
-// (the empty asm fences keep each group where the schedule puts it: without
-// them the SLP vectorizer packed the pairs into v_pk_fma_f32 and every group
-// sank below the tile's last MFMA, to the fail bits' use in the appends)
-__device__ __forceinline__ void t9_fence(float& v) { asm volatile("" : "+v"(v)); }
-__device__ __forceinline__ void t9_fence(uint32_t& v) { asm volatile("" : "+v"(v)); }
-template <int METRIC, int G>
-__device__ __forceinline__ void t9_epi_group(T9Epi& e, const f32x16 (&acc)[kT9RT]) {
-  constexpr int j = 2 * (7 - G);
-#pragma unroll
-  for (int t = 0; t < kT9RT; ++t) {
-    float v1 = fmaf(e.om[t], e.cb[0], acc[t][j + 1]);
-    v1 = fmaf(e.y1[t], e.cb[1], v1);
-    if constexpr (METRIC == 0) v1 = fmaf(e.y2[t], e.cb[2], v1);
-    float d1 = v1 + -kI8C0;
-    t9_fence(d1);
-    float v0 = fmaf(e.om[t], e.ca[0], acc[t][j]);
-    v0 = fmaf(e.y1[t], e.ca[1], v0);
-    if constexpr (METRIC == 0) v0 = fmaf(e.y2[t], e.ca[2], v0);
-    float d0 = v0 + -kI8C0;
-    t9_fence(d0);
-    e.fail[t] = __builtin_amdgcn_alignbit(e.fail[t], __float_as_uint(d1), 31);
-    e.fail[t] = __builtin_amdgcn_alignbit(e.fail[t], __float_as_uint(d0), 31);
-    t9_fence(e.fail[t]);
-  }
-}
-
-// the passing pairs of tile i-1 (parity P, rows r0 ..) into the query
-// segments: t8_epilogue's appends
-template <int METRIC>
-__device__ __forceinline__ void t9_epi_append(const T9Epi& e, const f32x16 (&acc)[kT9RT],
-                                              Img9Shared* sh, const FilterArgs& a, int64_t q0,
-                                              int64_t r0, int P, int qb, int l32,
-                                              uint32_t qlive) {
-  constexpr int SEG = kT8SEG;
-  uint32_t pm[kT9RT], any = 0u;
-#pragma unroll
-  for (int t = 0; t < kT9RT; ++t) {
-    const uint32_t force = e.om[t] != e.om[t] ? ~0u : 0u;
-    pm[t] = (~e.fail[t] | force) & sh->rkeep[P][t * 32 + l32] & qlive;
-    any |= pm[t];
-  }
-  if (__ballot(any != 0u) == 0ull) return;
-  static_for<kT9RT>([&](auto tc) {
-    constexpr int t = decltype(tc)::value;
-    uint32_t bits = pm[t];
-    if (__ballot(bits != 0u) == 0ull) return;
-    const int lr = t * 32 + (int)opaque((unsigned)l32);
-    const uint32_t irow = (uint32_t)(r0 + lr);
-    while (bits != 0u) {
-      const int j = __builtin_ctz(bits);
-      bits &= bits - 1u;
-      auto pick = [](float lo, float hi, uint32_t m) {
-        return __uint_as_float((__float_as_uint(hi) & m) | (__float_as_uint(lo) & ~m));
-      };
-      const uint32_t m0 = 0u - ((uint32_t)j & 1u), m1 = 0u - (((uint32_t)j >> 1) & 1u);
-      const uint32_t m2 = 0u - (((uint32_t)j >> 2) & 1u), m3 = 0u - (((uint32_t)j >> 3) & 1u);
-      float v8[8], v4[4], v2[2];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v8[i] = pick(acc[t][2 * i], acc[t][2 * i + 1], m0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v4[i] = pick(v8[2 * i], v8[2 * i + 1], m1);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) v2[i] = pick(v4[2 * i], v4[2 * i + 1], m2);
-      const float x = pick(v2[0], v2[1], m3);
-      const int qi = qb + (j & 3) + 8 * (j >> 2);
-      const uint32_t p = lds_add_rtn_u32(&sh->segc[qi], 1u);
-      if (p < (uint32_t)SEG) {
-        lds_write2_u32(&sh->sege[qi * SEG + p], __float_as_uint(x), irow);
-        if (p == (uint32_t)kT8Hi) lds_write1_u32(&sh->flush, 1u);
-      } else {
-        const int64_t gq = q0 + qi;
-        float lb, ub;
-        i8_bounds<METRIC>(x, e.om[t], e.y1[t], sh->rext[P][lr], sh->qinf[qi], a.d, lb, ub);
-        const uint32_t grow = sh->rrow[P][lr];
-        const uint32_t gp = atomicAdd(&a.count[gq * kCountStride], 1u);
-        if (gp < (uint32_t)a.cap) {
-          const size_t slot = (size_t)gq * a.cap + gp;
-          if (a.cand_ub != nullptr) {
-            a.cand[slot] = make_comp(lb, grow);
-            a.cand_ub[slot] = make_comp(ub, grow);
-          } else {
-            a.cand[slot] = make_comp(ub, grow);
-          }
-        }
-      }
-    }
-  });
-}
-
-// t8_flush over Img9Shared (the same segments, entries and bounds)
-template <int METRIC, bool RESET>
-__device__ __forceinline__ void t9_flush(Img9Shared* sh, const FilterArgs& a, int64_t q0, int tid) {
-  constexpr int SEG = kT8SEG;
-  for (int q = tid; q < fBQ; q += kT8Threads) {
-    const uint32_t n = sh->segc[q] < (uint32_t)SEG ? sh->segc[q] : (uint32_t)SEG;
-    sh->segn[q] = n;
-    sh->segbase[q] = n != 0u && q0 + q < a.nq ? atomicAdd(&a.count[(q0 + q) * kCountStride], n) : 0u;
-  }
-  __syncthreads();
-  for (int i = tid; i < fBQ * SEG; i += kT8Threads) {
-    const int q = i / SEG, j = i % SEG;
-    if ((uint32_t)j >= sh->segn[q]) continue;
-    const uint32_t p = sh->segbase[q] + (uint32_t)j;
-    if (p >= (uint32_t)a.cap) continue;
-    const uint2 e = sh->sege[i];
-    const int64_t row = (int64_t)e.y;
-    const f32x4 ri = *reinterpret_cast<const f32x4*>(a.rowinfo + row * kI8RowInfo);
-    const float y1 = METRIC == 1 ? ri[1] : METRIC == 2 ? ri[2] : ri[3];
-    float lb, ub;
-    i8_bounds<METRIC>(__uint_as_float(e.x), ri[0], y1, ri[1], sh->qinf[q], a.d, lb, ub);
-    const uint32_t grow = (uint32_t)a.row_base + perm_row(a.perm_a, a.n, row);
-    const size_t slot = (size_t)(q0 + q) * a.cap + p;
-    if (a.cand_ub != nullptr) {
-      a.cand[slot] = make_comp(lb, grow);
-      a.cand_ub[slot] = make_comp(ub, grow);
-    } else {
-      a.cand[slot] = make_comp(ub, grow);
-    }
-  }
-  if constexpr (RESET) {
-    __syncthreads();
-    for (int q = tid; q < fBQ; q += kT8Threads) sh->segc[q] = 0u;
-    if (tid == 0) sh->flush = 0u;
-    // (appends run at the end of the tile's k-loop, with no barrier after
-    // this one when a tile has one barrier interval: reset before any)
-    __syncthreads();
-  }
-}
-
-template <int METRIC, int NCH>
-__global__ void __launch_bounds__(kT8Threads, 2) filter_img9_kernel(FilterArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  Img9Shared* sh = reinterpret_cast<Img9Shared*>(smem);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, l32 = lane & 31;
-  const int64_t q0 = (int64_t)blockIdx.y * fBQ;
-  const int ksteps = (a.d + 31) / 32;
-  static_assert(NCH >= 1 && NCH <= kT8NC, "filter_img9_kernel: d <= 768");
-  const int64_t ntile32 = (a.n + 31) / 32;
-  const int64_t ntiles = a.num_tiles * kT9Sub;
-  auto tile_r0 = [&](int64_t ti) {
-    return (a.tile_start + (ti / kT9Sub) * a.tile_stride) * fBM + (ti % kT9Sub) * kT9BM;
-  };
-  if ((int64_t)blockIdx.x >= ntiles) return;
-  if (a.skip_full) {
-    bool full = true;
-    for (int q = tid; q < fBQ; q += kT8Threads)
-      if (q0 + q < a.nq && a.count[(q0 + q) * kCountStride] <= (uint32_t)a.cap) full = false;
-    if (__syncthreads_and(full)) return;
-  }
-  i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, kT8Threads);
-  for (int q = tid; q < fBQ; q += kT8Threads) sh->segc[q] = 0u;
-  if (tid < kT9BM) sh->rkeep[1][tid] = 0u;  // "tile -1": no pair passes
-  if (tid == 0) sh->flush = 0u;
-  i32x4 qa[kT8KS];
-  {
-    const unsigned char* qb = reinterpret_cast<const unsigned char*>(a.Qh + q0 * 32);
-    const int qchunks = a.dq / 64;
-    const int64_t qo = (int64_t)(wid * 32 + l32) * 64 + h * 16;
-#pragma unroll
-    for (int s = 0; s < kT8KS; ++s) {
-      const int c = s >> 1;
-      qa[s] = c < qchunks ? *reinterpret_cast<const i32x4*>(qb + (int64_t)c * a.qstride * 64 + qo +
-                                                             (s & 1) * 32)
-                          : i32x4(0);
-    }
-  }
-  __syncthreads();
-
-  // the ring: chunk c of a tile holds its 2 32-row tiles x k-steps 4 c .. 4 c
-  // + 3, KB (tt, kk) at (4 tt + kk) KB; wave w DMAs tt = w / 4, kk = w % 4
-  const int tt = wid >> 2, kk0 = wid & 3;
-  auto x_rsrc = [&](int64_t ti) {
-    const int64_t t32 = tile_r0(ti) / 32 + tt;
-    const int64_t live = (ti < ntiles && t32 < ntile32) ? 1 : 0;
-    const unsigned char* base = reinterpret_cast<const unsigned char*>(a.X) +
-                                (live ? t32 : 0) * (int64_t)ksteps * 1024;
-    const uint64_t xp = reinterpret_cast<uint64_t>(base);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)xp);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(xp >> 32));
-    const int nb = __builtin_amdgcn_readfirstlane((int)(live * ksteps * 1024));
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
-                                             nb, 0x00020000);
-  };
-  const uint32_t xl = (uint32_t)opaque((unsigned)lane) * 16u;
-  int64_t xt = blockIdx.x;
-  int xc = 0, wslot = 0;
-  __amdgpu_buffer_rsrc_t xr = x_rsrc(xt);
-  auto issue = [&]() {
-    unsigned char* st = sh->ring[wslot] + (tt * kT8CK + kk0) * 1024;
-    const int s = xc * kT8CK + kk0;  // (wave-uniform)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (i3_lds_ptr)st, 16, s < ksteps ? xl : 0x7fff0000u,
-                                             s * 1024, 0, 0);
-    if (++xc == NCH) {
-      xc = 0;
-      xt += gridDim.x;
-      xr = x_rsrc(xt);
-    }
-    wslot = wslot + 1 == kT9Slots ? 0 : wslot + 1;
-  };
-  constexpr bool PAIR = NCH % 2 == 0;
-  constexpr int kAhead = PAIR ? kT9Slots - 2 : kT9Slots - 1;
-#pragma unroll
-  for (int i = 0; i < kAhead; ++i) issue();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  f32x16 acc[2][kT9RT];
-  int rslot = 0;
-  const int qb = wid * 32 + 4 * h;
-  T9Epi epi;
-  int64_t prev_r0 = 0;
-  // The pass test over the tile's k-steps: the row terms at k-step 1, pair
-  // group g at k-step C(g), its query table entries read at L(g) = C(g) - 1
-  // (a k-step ahead: the entries' LDS reads then never make a group wait
-  // for the B fragments read after them) when the groups are two k-steps
-  // apart (d > 512), else at C(g); the appends after the last k-step's MFMAs.
-  constexpr int KT = NCH * kT8CK;
-  constexpr bool kPre = KT >= 20;
-  auto grp_at = [](int g) { return kPre ? 3 + g * (KT - 4) / 8 : 2 + g * (KT - 3) / 8; };
-  uint32_t qlive = 0u;  // (the wave's live queries: element j's bit)
-#pragma unroll
-  for (int j = 0; j < 16; ++j)
-    qlive |= (q0 + qb + (j & 3) + 8 * (j >> 2) < a.nq ? 1u : 0u) << j;
-  auto tile = [&](auto Pc, int64_t ti) {
-    constexpr int P = decltype(Pc)::value, Q = 1 - P;  // this tile's parity, the previous one's
-    const int64_t r0 = tile_r0(ti);
-    const int lr = tid & (kT9BM - 1);
-    f32x4 rsum = {};
-    uint32_t mword = ~0u;
-    static_for<NCH>([&](auto cc) {
-      constexpr int C = decltype(cc)::value;
-      if constexpr (PAIR) {
-        if constexpr (C % 2 == 0) {
-          i3_wait_barrier<(kAhead - 2) * kT9Dma>();
-          issue();
-          issue();
-        }
-      } else {
-        i3_wait_barrier<(kAhead - 1) * kT9Dma>();
-        issue();
-      }
-      if constexpr (C == 0) {
-        if (sh->flush) t9_flush<METRIC, true>(sh, a, q0, tid);
-        if constexpr (FX_T9_EPI == 1) {
-          t9_epi_begin<METRIC>(epi, sh, Q, l32);
-          static_for<8>([&](auto gc) {
-            t9_epi_load<decltype(gc)::value>(epi, sh, qb);
-            t9_epi_group<METRIC, decltype(gc)::value>(epi, acc[Q]);
-          });
-          t9_epi_append<METRIC>(epi, acc[Q], sh, a, q0, prev_r0, Q, qb, l32, qlive);
-          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-          if (sh->flush) t9_flush<METRIC, true>(sh, a, q0, tid);
-        }
-        const int64_t row = r0 + lr < a.n ? r0 + lr : a.n - 1;
-        rsum = *reinterpret_cast<const f32x4*>(a.rowinfo + row * kI8RowInfo);
-        if (a.mask != nullptr) mword = a.mask[perm_row(a.perm_a, a.n, row) >> 5];
-      }
-      constexpr int G = PAIR ? 2 : 1;
-      if constexpr (C % G == 0) {
-        constexpr int J = G * kT8CK;
-        typedef int i32x16 __attribute__((ext_vector_type(16)));
-        auto read_b = [&](i32x4 (&b)[kT9RT], auto jc) {
-          constexpr int j = decltype(jc)::value;
-          const int slot = rslot + j / kT8CK < kT9Slots ? rslot + j / kT8CK : rslot + j / kT8CK - kT9Slots;
-          const unsigned char* st = sh->ring[slot] + lane * 16 + (j % kT8CK) * 1024;
-#pragma unroll
-          for (int t = 0; t < kT9RT; ++t) b[t] = *reinterpret_cast<const i32x4*>(st + t * kT8CK * 1024);
-        };
-        auto mfma = [&](const i32x4 (&b)[kT9RT], auto jc) {
-          constexpr int j = decltype(jc)::value;
-          constexpr int s = (C + j / kT8CK) * kT8CK + j % kT8CK;
-#pragma unroll
-          for (int t = 0; t < kT9RT; ++t) {
-            // (the magic start value moved in per tile, not held in 16 registers)
-            const f32x16 cin = s == 0 ? f32x16(__uint_as_float(opaque(0x4B400000u))) : acc[P][t];
-            acc[P][t] = __builtin_bit_cast(
-                f32x16, __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], b[t],
-                                                              __builtin_bit_cast(i32x16, cin), 0, 0, 0));
-          }
-        };
-        i32x4 b0[kT9RT], b1[kT9RT];
-        read_b(b0, std::integral_constant<int, 0>{});
-        read_b(b1, std::integral_constant<int, 1>{});
-        __builtin_amdgcn_sched_barrier(0);
-        static_for<J>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          constexpr int s = C * kT8CK + j;  // k-step of the tile
-          if constexpr (j % 2 == 0)
-            mfma(b0, jc);
-          else
-            mfma(b1, jc);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (j + 2 < J) {
-            if constexpr (j % 2 == 0)
-              read_b(b0, std::integral_constant<int, j + 2>{});
-            else
-              read_b(b1, std::integral_constant<int, j + 2>{});
-          }
-          // tile i-1's pass test between this tile's MFMAs
-          if constexpr (FX_T9_EPI == 0 || FX_T9_EPI == 3) {
-            if constexpr (s == 1) t9_epi_begin<METRIC>(epi, sh, Q, l32);
-            static_for<8>([&](auto gc) {
-              constexpr int g = decltype(gc)::value;
-              if constexpr (grp_at(g) == s) {
-                if constexpr (!kPre) t9_epi_load<g>(epi, sh, qb);
-                t9_epi_group<METRIC, g>(epi, acc[Q]);
-              }
-              if constexpr (kPre && grp_at(g) - 1 == s) t9_epi_load<g>(epi, sh, qb);
-            });
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        });
-        rslot = rslot + G < kT9Slots ? rslot + G : rslot + G - kT9Slots;
-      }
-      if (C == NCH - 1 && tid < kT9BM) {
-        const int lr2 = (int)opaque((unsigned)tid);
-        const int64_t row = r0 + lr2;
-        const int64_t mrow = perm_row(a.perm_a, a.n, row < a.n ? row : a.n - 1);
-        const bool ok = row < a.n && ((mword >> (mrow & 31)) & 1u);
-        asm volatile("" ::"v"(rsum[0]), "v"(rsum[1]), "v"(rsum[2]), "v"(rsum[3]));
-        sh->rinfo[P][lr2] = rsum[0];
-        sh->rterm[P][lr2] = METRIC == 1 ? rsum[1] : METRIC == 2 ? rsum[2] : rsum[3];
-        sh->rext[P][lr2] = rsum[1];
-        sh->rrow[P][lr2] = (uint32_t)a.row_base + (row < a.n ? (uint32_t)mrow : 0u);
-        sh->rkeep[P][lr2] = ok ? 0xffffu : 0u;
-      }
-    });
-    // tile i-1's appends (its pass test is complete), then this tile's row
-    // notes are in LDS for the next tile's pass test, behind its first barrier
-    if constexpr (FX_T9_EPI == 0)
-      t9_epi_append<METRIC>(epi, acc[Q], sh, a, q0, prev_r0, Q, qb, l32, qlive);
-    if constexpr (FX_T9_EPI == 3) {  // (timing: the pass test without its appends)
-      if ((epi.fail[0] & epi.fail[1]) == 0x12345u) a.count[0] = 7;
-    }
-    if constexpr (FX_T9_EPI == 2) {  // (timing: the MFMAs kept live, no epilogue)
-      if (acc[P][0][0] == 1.2345f && acc[P][1][15] == 2.f) a.count[0] = 7;
-    }
-    prev_r0 = r0;
-  };
-  int last = -1;  // parity of the last tile this workgroup ran
-  for (int64_t ti = blockIdx.x; ti < ntiles; ti += 2 * (int64_t)gridDim.x) {
-    tile(std::integral_constant<int, 0>{}, ti);
-    last = 0;
-    if (ti + gridDim.x >= ntiles) break;
-    tile(std::integral_constant<int, 1>{}, ti + gridDim.x);
-    last = 1;
-  }
-  // the last tile's epilogue on its own, behind a barrier (its row notes and
-  // the accumulators of its final MFMAs)
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  auto final_epi = [&](auto Pc) {
-    constexpr int P = decltype(Pc)::value;
-    t9_epi_begin<METRIC>(epi, sh, P, l32);
-    static_for<8>([&](auto gc) {
-      t9_epi_load<decltype(gc)::value>(epi, sh, qb);
-      t9_epi_group<METRIC, decltype(gc)::value>(epi, acc[P]);
-    });
-    t9_epi_append<METRIC>(epi, acc[P], sh, a, q0, prev_r0, P, qb, l32, qlive);
-  };
-  if (FX_T9_EPI >= 2)
-    ;
-  else if (last == 0)
-    final_epi(std::integral_constant<int, 0>{});
-  else if (last == 1)
-    final_epi(std::integral_constant<int, 1>{});
-  __syncthreads();
-  t9_flush<METRIC, false>(sh, a, q0, tid);
-}
-
-template <int NCH>
-static const void* img9_fn(int metric) {
-  return metric == FX_METRIC_COS  ? (const void*)filter_img9_kernel<2, NCH>
-         : metric == FX_METRIC_IP ? (const void*)filter_img9_kernel<1, NCH>
-                                  : (const void*)filter_img9_kernel<0, NCH>;
-}
-
-// option "img8" 2, not all-pass, and more than two ring chunks per tile
-// (d > 256): with one barrier interval per tile the interleaved pass test
-// read stale accumulators (candidate counts off for d = 40 and 136; DESIGN.md
-// 3.6g)
-static bool img9_serves(const FilterArgs& a) {
-  return option(kOptImg8) == 2 && !a.all_pass && (a.d + 31) / 32 > 2 * kT8CK;
-}
-
-static int launch_img9(const FilterArgs& a, int metric, hipStream_t stream) {
-  const size_t smem = sizeof(Img9Shared);
-  const int nch = ((a.d + 31) / 32 + kT8CK - 1) / kT8CK;
-  const void* fn = nch <= 1   ? img9_fn<1>(metric)
-                   : nch == 2 ? img9_fn<2>(metric)
-                   : nch == 3 ? img9_fn<3>(metric)
-                   : nch == 4 ? img9_fn<4>(metric)
-                   : nch == 5 ? img9_fn<5>(metric)
-                              : img9_fn<6>(metric);
-  if (int rc = allow_lds(fn)) return rc;
-  int cus = 0;
-  int rc = device_cus(&cus);
-  if (rc) return rc;
-  const int64_t qtiles = (a.nq + fBQ - 1) / fBQ;
-  int64_t bx = (int64_t)cus;
-  if (bx > a.num_tiles * kT9Sub) bx = a.num_tiles * kT9Sub;
-  for (int64_t y0 = 0; y0 < qtiles; y0 += 65535) {
-    FilterArgs b = a;
-    const int64_t yn = (qtiles - y0) < 65535 ? (qtiles - y0) : 65535;
-    b.Qh = a.Qh + y0 * fBQ * 32;
-    b.qinfo = a.qinfo + y0 * fBQ * kI8QInfo;
-    b.thr = a.thr + y0 * fBQ;
-    b.count = a.count + y0 * fBQ * kCountStride;
-    b.cand = a.cand + y0 * fBQ * (int64_t)a.cap;
-    if (a.cand_ub) b.cand_ub = a.cand_ub + y0 * fBQ * (int64_t)a.cap;
-    b.nq = a.nq - y0 * fBQ;
-    void* args[] = {(void*)&b};
-    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bx, (unsigned)yn), dim3(kT8Threads), args,
-                                   smem, stream);
-    if (e != hipSuccess) {
-      set_error("filter_img9_kernel launch: %s", hipGetErrorString(e));
-      return FX_EHIP;
-    }
-  }
-  return check_launch("filter_img9_kernel");
-}
 #endif  // FX_FILTER_BQ >= 256
 
 #if FX_FILTER_BQ <= 128
@@ -4534,8 +4033,7 @@ int launch(const FilterArgs& a, int metric, hipStream_t stream) {
     return launch_img4(a, metric, stream);
 #elif FX_FILTER_IMG3
 #if FX_FILTER_BQ >= 256
-    if (img8_serves(a))
-      return img9_serves(a) ? launch_img9(a, metric, stream) : launch_img8(a, metric, stream);
+    if (img8_serves(a)) return launch_img8(a, metric, stream);
 #endif
     return launch_img3(a, metric, stream);
 #elif FX_FILTER_IMG2

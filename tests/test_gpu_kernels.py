@@ -866,10 +866,7 @@ def test_img8_queries_in_registers_equal_streamed_tile(eng, metric, d):
     pair), rows the image cannot represent and a mask.  600 000 rows make a
     three-phase plan (19, 293, 2 344 tiles): the all-pass first sample, F1
     and F2 all run the kernel (a one- or two-phase plan's all-pass F1 keeps
-    both bounds and stays with the appending kernels).  img8 2:
-    filter_img9_kernel (64-row tiles, the pass test of tile i-1 between tile
-    i's MFMAs) for every phase but the all-pass one: the same decisions, so
-    the same counts and bits."""
+    both bounds and stays with the appending kernels)."""
     n, k = 600_000, 30
     xh = _extreme_rows_cached(n, d, 81)
     x = torch.from_numpy(xh).to(eng.device)
@@ -883,7 +880,7 @@ def test_img8_queries_in_registers_equal_streamed_tile(eng, metric, d):
         for msk in (None, mask):
             dm = device_mask(msk, eng.device) if msk is not None else None
             got = {}
-            for img8 in (2, 1, 0):
+            for img8 in (1, 0):
                 with _lib.options(img8=img8, filter_image=8):
                     st = eng.scan(Shard(x, 0), q, m, k, dm)
                     counts, cap = eng.filter_counts(Shard(x, 0), nq, m, k, st)
@@ -893,9 +890,6 @@ def test_img8_queries_in_registers_equal_streamed_tile(eng, metric, d):
                     got[img8] = (counts, od.cpu().numpy(), orow.cpu().numpy())
             assert got[1][0] is not None
             np.testing.assert_array_equal(got[1][0], got[0][0], err_msg=f"nq {nq} mask {msk is not None}")
-            np.testing.assert_array_equal(got[2][0], got[0][0], err_msg=f"img9 nq {nq} mask {msk is not None}")
-            np.testing.assert_array_equal(got[2][2], got[0][2])
-            np.testing.assert_array_equal(got[2][1].view(np.uint32), got[0][1].view(np.uint32))
             np.testing.assert_array_equal(got[1][2], got[0][2])
             np.testing.assert_array_equal(got[1][1].view(np.uint32), got[0][1].view(np.uint32))
             with _lib.options(batched=0):

@@ -23,7 +23,7 @@ p.add_argument("--reps", type=int, default=30)
 p.add_argument("--nq", default="1,2,16,64,65,256", help="batch sizes (1-64: the q64i build)")
 p.add_argument("--img6", default="0,1,2", help="option img6 values")
 p.add_argument("--d", default="136,768")
-p.add_argument("--img8", default="1", help="option img8 values (2: filter_img9_kernel)")
+p.add_argument("--img8", default="1", help="option img8 values (0: off, 1: filter_img8_kernel)")
 p.add_argument("--metric", type=int, default=0, help="0 L2, 1 inner product, 2 cosine")
 p.add_argument("--n", type=int, default=70_000,
                help="rows (600000 and up: a 3-phase plan, every int8 phase in the batched kernels)")
