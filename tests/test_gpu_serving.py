@@ -38,8 +38,12 @@ SHARDS, PER_SHARD, D, K = 8, 500_000, 1536, 1000
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # median of 20 warm searches from a separate client process (5.3 ms before the
 # one-sync vector gather, profiles/r05_cfg4_serving_test.json; 3.74 ms after,
-# profiles/r05_cfg4_serving_test2.json)
-MEDIAN_MS_BOUND = 6.0
+# profiles/r05_cfg4_serving_test2.json; 4.70 ms on another box,
+# profiles/r06_cfg4_serving_test.json).  A guard against a gross regression
+# (round 4's in-process client measured 28 ms), set well above box-to-box
+# variation so that timing noise alone cannot fail this correctness test
+# (ADVICE r5); the median itself is recorded in gpurun_out/cfg4_serving_test.json.
+MEDIAN_MS_BOUND = 8.0
 # positions (of 3 queries x 1 000) whose id differs from the float64 oracle at
 # a near-tie (tests/parity.py's rule): float32 accumulation cannot order rows
 # whose 1536-d fp16 inner products differ by < 2e-6 relative.  Measured: 2
