@@ -417,3 +417,42 @@ def library_sha() -> str:
                 h.update(blk)
         _sha = h.hexdigest()[:16]
     return _sha
+
+
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+BUILD_INFO = os.path.join(HERE, "lib", "build_info.json")
+
+
+def sources_sha() -> str:
+    """SHA-256 (16 hex digits) over the library's sources (csrc/*.hip, *.h,
+    the Makefile and include/*.h, by name and content, sorted)."""
+    h = hashlib.sha256()
+    files = [os.path.join(CSRC, f) for f in os.listdir(CSRC)
+             if f.endswith((".hip", ".h")) or f == "Makefile"]
+    files += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith(".h")]
+    for p in sorted(files):
+        h.update(os.path.relpath(p, os.path.dirname(HERE)).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def build_info() -> dict:
+    """What ``__graft_entry__.build()`` recorded when it last ran make
+    (``build_mode``: "make"; ``build_exercised``: whether make recompiled
+    anything; the library and source hashes it produced), plus whether the
+    library loaded now is that build and the sources on disk are its sources.
+    Empty fields when no build() record exists (a library built by hand)."""
+    import json
+
+    rec = {}
+    try:
+        with open(BUILD_INFO) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        rec = {"build_mode": None, "build_exercised": None}
+    rec["library_is_recorded_build"] = rec.get("library_sha") == library_sha()
+    rec["sources_match"] = rec.get("sources_sha") == sources_sha()
+    return rec

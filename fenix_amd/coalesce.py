@@ -30,7 +30,9 @@ from typing import Any, Callable, Dict, Hashable, List, Optional, Tuple
 
 import numpy as np
 
-RunFn = Callable[[np.ndarray, int], Tuple[np.ndarray, np.ndarray]]
+# run(queries [n, d] float32, K) -> (dist [n, K], rows [n, K], ...): every
+# returned array is indexed [query, rank, ...] and sliced per request
+RunFn = Callable[[np.ndarray, int], Tuple[np.ndarray, ...]]
 
 
 def enabled() -> bool:
@@ -38,23 +40,23 @@ def enabled() -> bool:
 
 
 class _Request:
-    __slots__ = ("query", "k", "wake", "promoted", "dist", "rows", "error")
+    __slots__ = ("query", "k", "wake", "promoted", "parts", "error")
 
     def __init__(self, query: np.ndarray, k: int) -> None:
         self.query = query
         self.k = k
         self.wake = threading.Event()  # result ready, or promoted to leader
         self.promoted = False
-        self.dist: Optional[np.ndarray] = None
-        self.rows: Optional[np.ndarray] = None
+        self.parts: Optional[Tuple[np.ndarray, ...]] = None
         self.error: Optional[BaseException] = None
 
 
 class Coalescer:
     """Groups concurrent ``search(key, run, query, k)`` calls with equal keys.
 
-    ``run(queries [n, d] float32, K) -> (dist [n, K], rows [n, K])`` executes
-    one batch (host arrays).  A leader runs one batch — everything queued for
+    ``run(queries [n, d] float32, K) -> (dist [n, K], rows [n, K], ...)``
+    executes one batch (host arrays; any further arrays, such as the result
+    rows' vectors [n, K, d], are sliced per request the same way).  A leader runs one batch — everything queued for
     its key, at most ``max_batch`` — then hands leadership to the first
     request still queued, so no caller serves other callers' batches after
     its own result is ready."""
@@ -68,7 +70,7 @@ class Coalescer:
         self.requests = 0
 
     def search(self, key: Hashable, run: RunFn, query: np.ndarray, k: int
-               ) -> Tuple[np.ndarray, np.ndarray]:
+               ) -> Tuple[np.ndarray, ...]:
         req = _Request(np.ascontiguousarray(query, dtype=np.float32).reshape(-1), int(k))
         with self._lock:
             self.requests += 1
@@ -80,7 +82,7 @@ class Coalescer:
             self._lead_once(key, run)
         while True:
             req.wake.wait()
-            if req.promoted and req.dist is None and req.error is None:
+            if req.promoted and req.parts is None and req.error is None:
                 req.promoted = False
                 req.wake.clear()
                 self._lead_once(key, run)
@@ -88,7 +90,7 @@ class Coalescer:
             break
         if req.error is not None:
             raise req.error
-        return req.dist, req.rows
+        return req.parts
 
     def _lead_once(self, key: Hashable, run: RunFn) -> None:
         with self._lock:
@@ -110,10 +112,9 @@ class Coalescer:
     def _run(batch: List[_Request], run: RunFn) -> None:
         try:
             kmax = max(r.k for r in batch)
-            dist, rows = run(np.stack([r.query for r in batch]), kmax)
+            parts = run(np.stack([r.query for r in batch]), kmax)
             for i, r in enumerate(batch):
-                r.dist = dist[i : i + 1, : r.k]
-                r.rows = rows[i : i + 1, : r.k]
+                r.parts = tuple(p[i : i + 1, : r.k] for p in parts)
         except BaseException as e:  # every request of the batch sees the failure
             for r in batch:
                 r.error = e

@@ -914,6 +914,97 @@ def search_all(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: i
     return _search_all(shards, queries, metric, k, masks, counts)
 
 
+def gather_rows(shards: Sequence[Shard], rows: torch.Tensor) -> Optional[torch.Tensor]:
+    """The stored values of result rows, gathered on the device that holds
+    ``rows`` ([nq, K] int64 global row numbers, -1 = empty slot) ->
+    [nq, K, D] in the shards' dtype, or None when a shard lives on another
+    device (the caller then gathers on the host side, io.index._gather_vectors).
+
+    Queued on the stream right behind the search that produced ``rows``, so
+    the host enqueues it while the device still scans and the winning rows
+    come back with the distances in one D2H (index.py:166's take).  Empty
+    slots and rows outside every shard read a clamped row; the caller drops
+    the first and rejects the second (``check_rows``)."""
+    dev = rows.device
+    shards = [s for s in shards if s.n > 0]  # (an empty shard holds no result row)
+    if not shards or any(s.data.device != dev for s in shards):
+        return None
+    nq, kk = rows.shape
+    flat = rows.reshape(-1)
+    with torch.cuda.device(dev):
+        if len(shards) == 1:
+            s = shards[0]
+            local = (flat - s.row_base).clamp_(0, max(s.n - 1, 0))
+            return s.data.index_select(0, local).view(nq, kk, s.d)
+        bases = torch.tensor([s.row_base for s in shards], dtype=torch.int64).to(
+            dev, non_blocking=True)
+        which = torch.searchsorted(bases, flat, right=True) - 1
+        out = None
+        for i, s in enumerate(shards):
+            g = s.data.index_select(0, (flat - s.row_base).clamp_(0, max(s.n - 1, 0)))
+            out = g if out is None else torch.where((which == i).unsqueeze(1), g, out)
+        return out.view(nq, kk, shards[0].d)
+
+
+def check_rows(shards: Sequence[Shard], rows: np.ndarray) -> None:
+    """Every non-empty result row lies inside a shard, the shards in row order
+    (the assumption of gather_rows and io.index._gather_vectors)."""
+    bases = np.array([s.row_base for s in shards], dtype=np.int64)
+    ns = np.array([s.n for s in shards], dtype=np.int64)
+    if np.any(np.diff(bases) < 0):
+        raise ValueError("shards must be in row order")
+    r = rows[rows >= 0]
+    which = np.searchsorted(bases, r, side="right") - 1
+    if np.any(which < 0) or np.any(r - bases[np.maximum(which, 0)] >= ns[np.maximum(which, 0)]):
+        raise ValueError("a result row lies outside every shard")
+
+
+def _to_host(*ts: torch.Tensor) -> Tuple[np.ndarray, ...]:
+    """Device tensors -> host arrays: one pinned D2H each on the current
+    stream of their device, ONE synchronisation."""
+    outs = []
+    for t in ts:
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        h.copy_(t, non_blocking=True)
+        outs.append(h)
+    torch.cuda.current_stream(ts[0].device).synchronize()
+    return tuple(h.numpy() for h in outs)
+
+
+def search_host(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: int,
+                masks: Optional[Sequence[Optional[torch.Tensor]]] = None,
+                counts: Optional[Sequence[Optional[int]]] = None, gather: bool = False,
+                ) -> Tuple[np.ndarray, np.ndarray, Optional[np.ndarray]]:
+    """``search_all`` with the results on the host — what io.index.call
+    needs: (dist [nq, k] f32, rows [nq, k] i64, vectors [nq, k, D] or None).
+
+    With ``gather`` the result rows' stored values are gathered on the
+    device behind the search (``gather_rows``) and come back with the
+    distances and rows in one synchronisation (None when the shards span
+    devices).  A single unfiltered query goes through the serving coalescer
+    like ``search_all``."""
+    def run(qs: torch.Tensor, kk: int, ms=None, cs=None) -> Tuple[np.ndarray, ...]:
+        d, r = _search_all(shards, qs, metric, kk, ms, cs)
+        v = gather_rows(shards, r) if gather else None
+        if v is None:
+            return _to_host(d, r)
+        with torch.cuda.device(r.device):
+            return _to_host(d, r, v)
+
+    if (queries.shape[0] == 1 and masks is None and counts is None and coalesce.enabled()
+            and k <= _lib.load().fx_max_k()):
+        key = (tuple((id(s.data), s.data.data_ptr(), s.n, s.row_base) for s in shards), metric,
+               gather)
+        parts = coalesce.default().search(key, lambda qs, kk: run(torch.from_numpy(qs), kk),
+                                          queries.cpu().numpy(), k)
+    else:
+        parts = run(queries, k, masks, counts)
+    if len(parts) == 3:
+        check_rows(shards, parts[1])
+        return parts
+    return parts[0], parts[1], None
+
+
 # how many multi-device searches gathered their lists each way (bench.py, tests)
 GATHERS: Dict[str, int] = {"rccl": 0, "p2p": 0}
 _GATHERS_LOCK = threading.Lock()

@@ -143,7 +143,8 @@ def take_rows(data: pa.Table, rows: np.ndarray) -> pa.Table:
 
 
 def _gather_vectors(shards, rows: np.ndarray, type: pa.DataType,
-                    null: np.ndarray | None = None) -> pa.Array:
+                    null: np.ndarray | None = None,
+                    values: np.ndarray | None = None) -> pa.Array:
     """The k winning embeddings, read back from their HBM shards (they are the
     stored Arrow values, staged verbatim) instead of gathered from Arrow
     chunks (index.py:166's take): one H2D of (result position, local row)
@@ -155,11 +156,16 @@ def _gather_vectors(shards, rows: np.ndarray, type: pa.DataType,
     DESIGN §6.2).  ``null``: which
     result rows are null slots of the column; their stored values are
     gathered like any other (they were scanned) and the slot stays null, as
-    index.py:166's ``take`` keeps validity (tests/golden g7_nulls)."""
+    index.py:166's ``take`` keeps validity (tests/golden g7_nulls).
+    ``values``: the rows' stored values, already gathered on the device
+    behind the search (engine.search_host, one D2H with the distances); only
+    the Arrow array is built then."""
     d = _engine.list_size(type)
     _, tdt, ndt = _engine.value_dtype(type)
     m = rows.size
-    if m == 0 or not shards:
+    if values is not None:
+        out = np.ascontiguousarray(values).view(ndt).reshape(m, d)
+    elif m == 0 or not shards:
         out = np.empty((m, d), dtype=ndt)
     else:
         bases = np.array([s.row_base for s in shards], dtype=np.int64)
@@ -214,9 +220,10 @@ def _null_mask(col: pa.ChunkedArray) -> np.ndarray:
 
 
 def _take_columns(data: pa.Table, cols: List[str], rows: np.ndarray, column: str, shards,
-                  version) -> pa.Table:
+                  version, values: np.ndarray | None = None) -> pa.Table:
     """select(cols).take(rows) without Table.take's concatenation of the whole
-    chunked vector column (index.py:166; 0.75 s per 1M x 768 measured)."""
+    chunked vector column (index.py:166; 0.75 s per 1M x 768 measured);
+    ``values``: the vector column's rows, gathered on the device already."""
     arrays = []
     for c in cols:
         col = data.column(c)
@@ -225,7 +232,7 @@ def _take_columns(data: pa.Table, cols: List[str], rows: np.ndarray, column: str
             if col.null_count:
                 null = (_resident.null_mask(version, c, col) if version is not None
                         else _null_mask(col))[rows]
-            arrays.append(_gather_vectors(shards, rows, col.type, null))
+            arrays.append(_gather_vectors(shards, rows, col.type, null, values))
         elif version is None:
             arrays.append(_take_chunked(col, rows))
         else:
@@ -464,12 +471,15 @@ def call(
     base_cols = [c for c in dict.fromkeys(select) if c != DIST_COL]
 
     if maxval is not None and n_rows > maxval:
-        dist, rows = _engine.search_all(shards, qt, m, int(maxval), masks, counts)
-        dist = dist[0].cpu().numpy()
-        rows = rows[0].cpu().numpy()
+        # the k winning vectors are gathered on the device behind the scan and
+        # come back with the distances (one synchronisation)
+        dist, rows, vecs = _engine.search_host(shards, qt, m, int(maxval), masks, counts,
+                                               gather=column in base_cols)
+        dist, rows = dist[0], rows[0]
         keep = rows >= 0
         dist, rows = dist[keep], rows[keep]
-        out = _take_columns(data, base_cols, rows, column, shards, version)
+        vecs = vecs[0][keep] if vecs is not None else None
+        out = _take_columns(data, base_cols, rows, column, shards, version, vecs)
     else:
         dist = _engine.distances_all(shards, qt, m, masks)[0]
         out = data.select(base_cols)

@@ -71,6 +71,9 @@ def main() -> None:
     p.add_argument("--root", default="", help="server root directory (default: a temp dir)")
     p.add_argument("--no-coalesce", action="store_true",
                    help="serve every request alone (FENIX_AMD_COALESCE=0)")
+    p.add_argument("--canned", action="store_true",
+                   help="the server answers every search with the first search's result "
+                        "table (no io.index.call): the Flight + gRPC floor above the engine")
     p.add_argument("--client", action="store_true")
     p.add_argument("--port", type=int, default=0)
     p.add_argument("--source", default="bench/table", help="client: the table to search")
@@ -119,6 +122,17 @@ def main() -> None:
     else:
         writer.make_table("bench/table", reader)
     t_put = time.perf_counter() - t0
+    if a.canned:
+        from fenix_amd.io import index as _index
+
+        real, memo = _index.call, {}
+
+        def canned(*args, **kw):
+            if "t" not in memo:
+                memo["t"] = real(*args, **kw)
+            return memo["t"]
+
+        _index.call = canned
     cmd = [sys.executable, os.path.abspath(__file__), "--client", "--port", str(port),
            "--d", str(a.d), "--k", str(a.k), "--metric", a.metric, "--dtype", a.dtype,
            "--reps", str(a.reps)]
@@ -152,6 +166,7 @@ def main() -> None:
         "aggregate_searches_per_s": a.clients * a.reps / sum(
             np.sum(r["lat_ms"]) / 1e3 / a.clients for r in results) if a.clients > 1 else None,
         "wall_s_incl_client_start": wall,
+        "canned_reply": a.canned,
         "coalesce": coalesce.enabled(),
         "coalesced": coalesce.describe(coalesce.default()),
     }), flush=True)

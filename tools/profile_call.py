@@ -5,7 +5,7 @@
     python tools/profile_call.py --n 4000000 --shards 8 --batch 100000 --json out.json
 
 Prints the median of ``--reps`` warm calls, a per-phase breakdown (each phase
-wrapped with a wall clock; ``search_all`` ends with the result's D2H, which
+wrapped with a wall clock; ``search_host`` ends with the result's D2H, which
 waits for the GPU) and a cProfile listing.  ``--cpu-load`` runs the oracle's
 16-thread OpenMP scan between calls, as tests/test_gpu_serving.py does, to
 measure what that does to the next call.
@@ -95,7 +95,7 @@ def main() -> None:
         return fn
 
     for mod, name in ((index._resident, "sources"), (index._resident, "shards"),
-                      (index, "_target_values"), (index._engine, "search_all"),
+                      (index, "_target_values"), (index._engine, "search_host"),
                       (index, "_take_columns"), (index, "_gather_vectors"),
                       (index, "_take_chunked")):
         clocked(mod, name)

@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round-6 measurement steps on one GPU box, chosen by name:
+#   bash tools/r06_job.sh bench flightprof flight k1000 ...
+# bench      default bench.py line (configs[1] headline + legs)
+# flightprof io.index.call phase breakdown + cProfile at configs[1]'s shape
+# flight     Flight.search from a torch-free client at configs[1]'s shape
+# k1000      one configs[4] shard (6.25M x 1536 f16 IP k=1000): exact scan vs
+#            the int8 image with i8_max_k raised (candidate counts, time)
+# Each GPU step has its own limit; the first failure ends the script.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out/r06
+export TMPDIR=/tmp
+run() {
+  local name=$1 secs=$2
+  shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/r06/$name.log" 2>&1
+  local rc=$?
+  echo "   $name rc=$rc"
+  tail -n 4 "gpurun_out/r06/$name.log"
+  [ $rc -eq 0 ] || exit $rc
+}
+TESTS=${TESTS:-tests}
+for step in "$@"; do
+  case $step in
+    bench) run bench 300 python -u bench.py ;;
+    flightprof) run flightprof 600 python -u tools/profile_call.py --n 10000000 --d 768 --dtype f32 \
+        --metric l2 --k 100 --batch 1000 --reps 30 --json gpurun_out/r06/flightprof.json ;;
+    flight) run flight 600 python -u tools/bench_flight.py --n 10000000 --d 768 --k 100 --metric l2 \
+        --direct --reps 60 ;;
+    flightc) run flightc 600 python -u tools/bench_flight.py --n 10000000 --d 768 --k 100 --metric l2 \
+        --direct --reps 60 --canned ;;
+    tests) run tests 900 python -u -m pytest $TESTS -m gpu -x -v -p no:cacheprovider --timeout 300 \
+        --timeout-method thread ;;
+    flight0) run flight0 300 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 --reps 60 ;;
+    k1000) run k1000a 300 python -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
+        --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024
+      run k1000b 300 python -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
+        --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024 --query near ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done"
