@@ -41,9 +41,9 @@ static std::mutex g_mu;
 static const char* const kOptNames[kOptCount] = {
     "batched", "batch_min_queries", "batch_cap", "batch_sample_ratio",
     "force_fallback", "scan_interleave", "q8_dma", "filter_image", "batch_ub_test",
-    "single_query_image", "i8_max_k", "img6", "img8"};
+    "single_query_image", "i8_max_k", "img6", "img8", "i8_sample_ratio", "i8_grow_ratio"};
 static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}, {8}, {1}, {1},
-                                                 {256}, {1}, {1}};
+                                                 {256}, {1}, {1}, {8}, {16}};
 
 int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
 
@@ -192,9 +192,8 @@ static constexpr int64_t kLargeMaxK = 0x7fffffffll;
 // single-query scan, gated on the device (fx_knn_reduce: no host sync).
 static constexpr int64_t kListLen = 4096;  // candidate buffer viewed as lists
 // int8 filter image (filter_phases_i8): the final pass's sample F1 takes
-// every kI8SampleRatio-th tile, the samples before it grow by kI8GrowRatio
-static constexpr int64_t kI8SampleRatio = 8;
-static constexpr int64_t kI8GrowRatio = 16;
+// every r1-th tile, the samples before it grow by r2 (options
+// "i8_sample_ratio", default 8, and "i8_grow_ratio", default 16)
 
 struct BatchLayout {
   int64_t cap = 0, tiles = 0, nq_pad = 0;
@@ -205,7 +204,7 @@ struct BatchLayout {
   int64_t start[16], stride[16], num[16];
   MergePlan merge;
   size_t off_qnorm, off_thr, off_count, off_cand, off_merge, off_cand_ub, off_qh, off_qinfo,
-      off_topd, off_topr, total;
+      off_topd, off_topr, off_prune, total;
 };
 
 // The fp16-MFMA filter (knn_filter.hip).  Diagnostic builds keep the
@@ -297,6 +296,9 @@ static int plan_batched(int64_t n, int64_t d, int dtype, int64_t nq, int64_t k, 
     b->off_topr = off;
     off += align256((size_t)nq * k * 8);
   }
+  // the selects' prune scratch (int8 plans at large k: select_prune_lists)
+  b->off_prune = off;
+  if (b->img8) off += align256(select_prune_bytes(nq, k, b->cap));
   b->total = off;
   return FX_OK;
 }
@@ -691,9 +693,10 @@ static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, cons
   };
   // the exact k-th of the k best upper bounds in `keys` -> thr (one fused
   // launch when the buffer fits one workgroup's LDS)
+  uint64_t* prune = reinterpret_cast<uint64_t*>(w + b.off_prune);
   auto exact_threshold = [&](const uint64_t* keys, bool zero) {
     return launch_exact_threshold(X, dtype, n, (int)d, row_base, Q, qnorm, nq, keys, b.cap, count,
-                                  zero, (int)k, metric, thr, st);
+                                  zero, (int)k, metric, thr, st, prune);
   };
   const int m = b.nphases;
   for (int ph = 0; ph + 2 < m; ++ph) {  // sampling phases: thresholds only
@@ -704,7 +707,8 @@ static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, cons
     if (rc) return rc;
     // (both reset the counts they read: the next phase appends from 0)
     rc = ph + 3 == m ? exact_threshold(cand, true)
-                     : launch_sample_threshold(cand, nq, b.cap, count, true, (int)k, thr, st);
+                     : launch_sample_threshold(cand, nq, b.cap, count, true, (int)k, thr, st,
+                                               prune);
     if (rc) return rc;
   }
   // F1: the last sample's tiles (with one phase: every tile), both bounds
@@ -944,8 +948,10 @@ static int scan_impl(const void* corpus, int dtype, int64_t n, int64_t d, int64_
       if (img && img8) {  // int8 image: denser samples (filter_phases)
         BatchLayout b = s.batch;
         const int64_t rmax = b.cap / (4 * k);
-        int64_t r1 = rmax < kI8SampleRatio ? rmax : kI8SampleRatio;
-        int64_t r2 = rmax < kI8GrowRatio ? rmax : kI8GrowRatio;
+        const int64_t o1 = option(kOptI8SampleRatio) >= 2 ? option(kOptI8SampleRatio) : 2;
+        const int64_t o2 = option(kOptI8GrowRatio) >= 2 ? option(kOptI8GrowRatio) : 2;
+        int64_t r1 = rmax < o1 ? rmax : o1;
+        int64_t r2 = rmax < o2 ? rmax : o2;
         const int64_t v = option(kOptBatchRatio);  // test switch: any ratio up to rmax
         if (v >= 2) r1 = r2 = v < rmax ? v : rmax;
         rc = plan_phases_i8(&b, filter_tile_rows(dtype), r1, r2);
@@ -1171,11 +1177,12 @@ static int reduce_impl(const void* corpus, int dtype, int64_t n, int64_t d, int6
                        w + s.single_off, st, &lists);
     if (rc) return rc;
     return launch_final_select(cand, nq, b.cap, count, (int)k, out_dist, out_row, lists,
-                               s.scan.nlists * k, gate_cap, st);
+                               s.scan.nlists * k, gate_cap, st,
+                               reinterpret_cast<uint64_t*>(w + b.off_prune));
   }
   // (the fallback gate reads the counts next: kept)
   rc = b.img8 ? launch_final_select(cand, nq, b.cap, count, (int)k, out_dist, out_row, nullptr, 0,
-                                    0, st)
+                                    0, st, reinterpret_cast<uint64_t*>(w + b.off_prune))
               : run_merge(b.merge, cand, nq, k, w + b.off_merge, out_dist, out_row, st, nullptr,
                           nullptr, 0, count);
   if (rc) return rc;

@@ -31,6 +31,8 @@ enum Option : int {
   kOptI8MaxK,       // largest k an int8 filter image serves
   kOptImg6,         // int8 images: resident-query-slice kernel (1: <= 128 queries, 2: all, 0: off)
   kOptImg8,         // int8 images: queries-in-registers kernel for > 128 queries, d <= 768 (0: off)
+  kOptI8SampleRatio,  // int8 images: F1 holds every r1-th tile (filter_phases_i8)
+  kOptI8GrowRatio,    // int8 images: the samples before F1 shrink by r2 each
   kOptCount
 };
 int64_t option(Option o);
@@ -152,21 +154,28 @@ int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_bas
 // run_merge (top-k by key of each query's first count[q] entries of keys
 // [nq][cap]) + launch_exact_kth in one launch, any cap (knn_batch.hip
 // select_kernel, streaming over LDS-sized chunks)
+// prune (these three): scratch of select_prune_bytes(nq, k, cap) or null;
+// a plan that prunes (k ~ 1 000 over a large buffer) first keeps the k
+// smallest of every LDS-sized slice in parallel (select_kernel MODE 3)
+int select_prune_lists(int64_t k, int64_t cap);
+size_t select_prune_bytes(int64_t nq, int64_t k, int64_t cap);
 int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t row_base,
                            const float* Q, const float* qnorm, int64_t nq, const uint64_t* keys,
                            int64_t cap, uint32_t* count, bool zero_count, int k, int metric,
-                           uint64_t* thr, hipStream_t stream);
+                           uint64_t* thr, hipStream_t stream, uint64_t* prune = nullptr);
 // thr[q] = min(thr[q], the k-th smallest of the query's first count[q] keys)
 // when it has at least k (run_merge's threshold-only level, any cap)
 int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint32_t* count,
-                            bool zero_count, int k, uint64_t* thr, hipStream_t stream);
+                            bool zero_count, int k, uint64_t* thr, hipStream_t stream,
+                            uint64_t* prune = nullptr);
 // the final top-k of each query's first count[q] exact composites of keys
 // [nq][cap], sorted and decoded (run_merge's last level, one workgroup per
 // query, any cap); a query whose count exceeds alt_gate selects from its
 // alt_m entries of alt ([nq][alt_m], the overflow fallback scan's lists)
 int launch_final_select(const uint64_t* keys, int64_t nq, int64_t cap, const uint32_t* count,
                         int k, float* out_dist, int64_t* out_row, const uint64_t* alt,
-                        int64_t alt_m, int64_t alt_gate, hipStream_t stream);
+                        int64_t alt_m, int64_t alt_gate, hipStream_t stream,
+                        uint64_t* prune = nullptr);
 
 // Batched filter on the fp16 matrix cores (knn_filter.hip): appends every
 // (row, query) whose rigorous lower bound reaches the query's threshold.

@@ -598,7 +598,15 @@ int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_bas
 //     overflowed the buffer) selects from its alt_m entries of alt instead
 //     (the overflow fallback scan's lists, [nq][alt_m]);
 //   MODE 2 (sample threshold): thr[q] = min(thr[q], the k-th smallest key)
-//     when there are at least k (run_merge's threshold-only level).
+//     when there are at least k (run_merge's threshold-only level);
+//   MODE 3 (prune, before a MODE 0/1/2 launch over many candidates): grid
+//     (pre_p, nq), workgroup p keeps the k smallest of the query's entries
+//     [p pre_s, (p + 1) pre_s) and writes them (kEmpty-padded) to
+//     pre[q][p][k]; the MODE 0/1/2 launch given the same pre then selects
+//     from the ceil(m / pre_s) k-lists of pre instead of streaming all m
+//     entries through one workgroup (k = 1 000, ~100 K candidates: the
+//     one-workgroup select took 160-230 us).  Not for the overflow path's
+//     alt lists.
 // zero_count resets the count once every thread has read it.
 #ifndef FX_SELECT_THREADS
 #define FX_SELECT_THREADS 1024
@@ -612,7 +620,8 @@ __global__ void __launch_bounds__(kSelectThreads)
                   const uint64_t* __restrict__ keys, int64_t cap, uint32_t* __restrict__ count,
                   int zero_count, int k, int P2, uint64_t* __restrict__ thr,
                   float* __restrict__ out_dist, int64_t* __restrict__ out_row,
-                  const uint64_t* __restrict__ alt, int64_t alt_m, int64_t alt_gate) {
+                  const uint64_t* __restrict__ alt, int64_t alt_m, int64_t alt_gate,
+                  uint64_t* __restrict__ pre, int pre_p, int64_t pre_s) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   MergeShared* ms = reinterpret_cast<MergeShared*>(smem);
   uint64_t* res = reinterpret_cast<uint64_t*>(smem + sizeof(MergeShared));
@@ -622,13 +631,53 @@ __global__ void __launch_bounds__(kSelectThreads)
   const uint32_t c = count[q * kCountStride];
   int64_t m = (int64_t)c < cap ? (int64_t)c : cap;
   const uint64_t* src = keys + q * cap;
+  bool use_alt = false;
   if (MODE == 1 && alt != nullptr && (int64_t)c > alt_gate) {
     m = alt_m;
     src = alt + q * alt_m;
+    use_alt = true;
+  }
+  if constexpr (MODE == 3) {
+    const int64_t lo = (int64_t)blockIdx.x * pre_s;
+    if (use_alt || lo >= m) return;  // (uniform)
+    const int cnt = (int)((m - lo) < pre_s ? (m - lo) : pre_s);
+    uint64_t* out = pre + (q * pre_p + blockIdx.x) * (int64_t)k;
+    block_reset(ms);
+    __syncthreads();
+    uint64_t v_or = 0, v_and = ~0ull;
+    for (int base = tid; base < cnt; base += kSelectThreads * 8) {
+      uint64_t e[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = base + j * kSelectThreads;
+        e[j] = i < cnt ? src[lo + i] : kEmpty;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = base + j * kSelectThreads;
+        if (i < cnt) {
+          s[i] = e[j];
+          v_or |= e[j];
+          v_and &= e[j];
+        }
+      }
+    }
+    block_or_and(v_or, v_and, ms);
+    __syncthreads();
+    if (cnt > k) {
+      block_keep_k<kSelectThreads>(s, cnt, k, out, ms);
+    } else {
+      for (int i = tid; i < k; i += kSelectThreads) out[i] = i < cnt ? s[i] : kEmpty;
+    }
+    return;
   }
   __syncthreads();
   if (zero_count && tid == 0) count[q * kCountStride] = 0u;
   if (MODE != 1 && m < k) return;  // (uniform) fewer than k candidates: no threshold
+  if (pre != nullptr && !use_alt) {  // the pruned k-lists of the same entries (MODE 3)
+    src = pre + q * pre_p * (int64_t)k;
+    m = (m + pre_s - 1) / pre_s * k;
+  }
   int nres = 0;
   const int64_t chunk = kSelectEntries - k;
   for (int64_t off = 0; off < m || (off == 0 && m == 0); off += chunk) {  // (uniform)
@@ -730,12 +779,26 @@ __global__ void __launch_bounds__(kSelectThreads)
   }
 }
 
+// The prune pass (select_kernel MODE 3): slices of kSelectEntries, used for
+// k >= kPruneMinK when the buffer holds more than two slices (int8-image
+// plans at k ~ 1 000: ~100 K candidates per query).  k-lists per query, 0 = off.
+constexpr int kPruneMinK = 512;
+int select_prune_lists(int64_t k, int64_t cap) {
+  if (k < kPruneMinK || cap <= 2 * (int64_t)kSelectEntries) return 0;
+  return (int)((cap + kSelectEntries - 1) / kSelectEntries);
+}
+
+size_t select_prune_bytes(int64_t nq, int64_t k, int64_t cap) {
+  return (size_t)nq * (size_t)select_prune_lists(k, cap) * (size_t)k * 8;
+}
+
 template <typename T, int MODE>
-static int launch_select_t(const T* X, int64_t n, int d, int64_t row_base, const float* Q,
-                           const float* qnorm, int64_t nq, const uint64_t* keys, int64_t cap,
-                           uint32_t* count, int zero, int k, int metric, uint64_t* thr,
-                           float* out_dist, int64_t* out_row, const uint64_t* alt,
-                           int64_t alt_m, int64_t alt_gate, hipStream_t stream) {
+static int launch_select_one(const T* X, int64_t n, int d, int64_t row_base, const float* Q,
+                             const float* qnorm, int64_t nq, const uint64_t* keys, int64_t cap,
+                             uint32_t* count, int zero, int k, int metric, uint64_t* thr,
+                             float* out_dist, int64_t* out_row, const uint64_t* alt,
+                             int64_t alt_m, int64_t alt_gate, uint64_t* pre, int pre_p,
+                             hipStream_t stream) {
   const void* fn = metric == FX_METRIC_COS  ? (const void*)select_kernel<T, 2, MODE>
                    : metric == FX_METRIC_IP ? (const void*)select_kernel<T, 1, MODE>
                                             : (const void*)select_kernel<T, 0, MODE>;
@@ -743,6 +806,8 @@ static int launch_select_t(const T* X, int64_t n, int d, int64_t row_base, const
   int P2 = 1;
   while (P2 < k) P2 <<= 1;
   const size_t smem = sizeof(MergeShared) + ((size_t)P2 + kSelectEntries) * 8;
+  const int64_t pre_s = kSelectEntries;
+  const unsigned gx = MODE == 3 ? (unsigned)pre_p : 1u;
   for (int64_t q0 = 0; q0 < nq; q0 += 65535) {
     const int64_t qn = (nq - q0) < 65535 ? (nq - q0) : 65535;
     const T* x = X;
@@ -754,11 +819,13 @@ static int launch_select_t(const T* X, int64_t n, int d, int64_t row_base, const
     float* od = out_dist != nullptr ? out_dist + q0 * k : nullptr;
     int64_t* orow = out_row != nullptr ? out_row + q0 * k : nullptr;
     const uint64_t* aq = alt != nullptr ? alt + q0 * alt_m : nullptr;
-    void* args[] = {(void*)&x,   (void*)&n,   (void*)&d,     (void*)&row_base, (void*)&qv,
-                    (void*)&qnm, (void*)&kq,  (void*)&cap,   (void*)&cq,       (void*)&zero,
-                    (void*)&k,   (void*)&P2,  (void*)&tq,    (void*)&od,       (void*)&orow,
-                    (void*)&aq,  (void*)&alt_m, (void*)&alt_gate};
-    hipError_t e = hipLaunchKernel(fn, dim3(1, (unsigned)qn), dim3(kSelectThreads), args, smem,
+    uint64_t* pq = pre != nullptr ? pre + q0 * (int64_t)pre_p * k : nullptr;
+    void* args[] = {(void*)&x,   (void*)&n,     (void*)&d,     (void*)&row_base, (void*)&qv,
+                    (void*)&qnm, (void*)&kq,    (void*)&cap,   (void*)&cq,       (void*)&zero,
+                    (void*)&k,   (void*)&P2,    (void*)&tq,    (void*)&od,       (void*)&orow,
+                    (void*)&aq,  (void*)&alt_m, (void*)&alt_gate, (void*)&pq,    (void*)&pre_p,
+                    (void*)&pre_s};
+    hipError_t e = hipLaunchKernel(fn, dim3(gx, (unsigned)qn), dim3(kSelectThreads), args, smem,
                                    stream);
     if (e != hipSuccess) {
       set_error("select_kernel launch: %s", hipGetErrorString(e));
@@ -768,10 +835,32 @@ static int launch_select_t(const T* X, int64_t n, int d, int64_t row_base, const
   return check_launch("select_kernel");
 }
 
+// One select (MODE 0/1/2); with a prune scratch (select_prune_bytes, may be
+// null) and a plan that prunes (select_prune_lists), the MODE 3 pass first.
+template <typename T, int MODE>
+static int launch_select_t(const T* X, int64_t n, int d, int64_t row_base, const float* Q,
+                           const float* qnorm, int64_t nq, const uint64_t* keys, int64_t cap,
+                           uint32_t* count, int zero, int k, int metric, uint64_t* thr,
+                           float* out_dist, int64_t* out_row, const uint64_t* alt,
+                           int64_t alt_m, int64_t alt_gate, hipStream_t stream,
+                           uint64_t* pre = nullptr) {
+  const int pre_p = pre != nullptr ? select_prune_lists(k, cap) : 0;
+  if (pre_p == 0) pre = nullptr;
+  if (pre != nullptr) {
+    int rc = launch_select_one<T, 3>(X, n, d, row_base, Q, qnorm, nq, keys, cap, count, 0, k,
+                                     metric, thr, out_dist, out_row, alt, alt_m, alt_gate, pre,
+                                     pre_p, stream);
+    if (rc) return rc;
+  }
+  return launch_select_one<T, MODE>(X, n, d, row_base, Q, qnorm, nq, keys, cap, count, zero, k,
+                                    metric, thr, out_dist, out_row, alt, alt_m, alt_gate, pre,
+                                    pre_p, stream);
+}
+
 int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t row_base,
                            const float* Q, const float* qnorm, int64_t nq, const uint64_t* keys,
                            int64_t cap, uint32_t* count, bool zero_count, int k, int metric,
-                           uint64_t* thr, hipStream_t stream) {
+                           uint64_t* thr, hipStream_t stream, uint64_t* prune) {
   if (k > kSelectMaxK || k > cap) {
     set_error("exact threshold: k %d beyond cap %lld", k, (long long)cap);
     return FX_EUNSUPPORTED;
@@ -779,26 +868,27 @@ int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t r
   if (dtype == FX_DTYPE_F16)
     return launch_select_t<_Float16, 0>(reinterpret_cast<const _Float16*>(X), n, d, row_base, Q,
                                         qnorm, nq, keys, cap, count, zero_count ? 1 : 0, k, metric,
-                                        thr, nullptr, nullptr, nullptr, 0, 0, stream);
+                                        thr, nullptr, nullptr, nullptr, 0, 0, stream, prune);
   return launch_select_t<float, 0>(reinterpret_cast<const float*>(X), n, d, row_base, Q, qnorm, nq,
                                    keys, cap, count, zero_count ? 1 : 0, k, metric, thr, nullptr,
-                                   nullptr, nullptr, 0, 0, stream);
+                                   nullptr, nullptr, 0, 0, stream, prune);
 }
 
 int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint32_t* count,
-                            bool zero_count, int k, uint64_t* thr, hipStream_t stream) {
+                            bool zero_count, int k, uint64_t* thr, hipStream_t stream,
+                            uint64_t* prune) {
   if (k > kSelectMaxK) {
     set_error("sample threshold: k %d too large", k);
     return FX_EUNSUPPORTED;
   }
   return launch_select_t<float, 2>(nullptr, 0, 1, 0, nullptr, nullptr, nq, keys, cap, count,
                                    zero_count ? 1 : 0, k, FX_METRIC_L2, thr, nullptr, nullptr,
-                                   nullptr, 0, 0, stream);
+                                   nullptr, 0, 0, stream, prune);
 }
 
 int launch_final_select(const uint64_t* keys, int64_t nq, int64_t cap, const uint32_t* count,
                         int k, float* out_dist, int64_t* out_row, const uint64_t* alt,
-                        int64_t alt_m, int64_t alt_gate, hipStream_t stream) {
+                        int64_t alt_m, int64_t alt_gate, hipStream_t stream, uint64_t* prune) {
   if (k > kSelectMaxK) {
     set_error("final select: k %d too large", k);
     return FX_EUNSUPPORTED;
@@ -806,7 +896,7 @@ int launch_final_select(const uint64_t* keys, int64_t nq, int64_t cap, const uin
   // (MODE 1 reads no rows: the keys are exact composites already)
   return launch_select_t<float, 1>(nullptr, 0, 1, 0, nullptr, nullptr, nq, keys, cap,
                                    const_cast<uint32_t*>(count), 0, k, FX_METRIC_L2, nullptr,
-                                   out_dist, out_row, alt, alt_m, alt_gate, stream);
+                                   out_dist, out_row, alt, alt_m, alt_gate, stream, prune);
 }
 
 }  // namespace fx

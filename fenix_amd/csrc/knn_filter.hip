@@ -4506,11 +4506,12 @@ uint64_t image8_perm(int64_t n) {
   return a % (uint64_t)n;
 }
 
-// One workgroup per query (launch_overflow_gate, fx_internal.h)
-__global__ void __launch_bounds__(256) overflow_gate_kernel(const uint64_t* __restrict__ cand,
-                                                            uint32_t* __restrict__ count,
-                                                            const uint64_t* __restrict__ thr,
-                                                            int cap, int64_t num, int64_t den) {
+// One workgroup per query (launch_overflow_gate, fx_internal.h), 8 loads in
+// flight per thread (k = 1 000: ~50 K F1 candidates per query, 63 -> ~10 us)
+constexpr int kGateThreads = 1024;
+__global__ void __launch_bounds__(kGateThreads) overflow_gate_kernel(
+    const uint64_t* __restrict__ cand, uint32_t* __restrict__ count,
+    const uint64_t* __restrict__ thr, int cap, int64_t num, int64_t den) {
   const int64_t q = blockIdx.x;
   __shared__ uint32_t tot;
   const uint32_t c = count[q * kCountStride];
@@ -4520,7 +4521,16 @@ __global__ void __launch_bounds__(256) overflow_gate_kernel(const uint64_t* __re
   const uint32_t t = (uint32_t)(thr[q] >> 32);
   const uint64_t* cq = cand + q * (int64_t)cap;
   uint32_t mine = 0u;
-  for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) mine += (uint32_t)(cq[i] >> 32) <= t;
+  for (uint32_t b = threadIdx.x; b < c; b += kGateThreads * 8) {
+    uint64_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = b + j * kGateThreads;
+      e[j] = i < c ? cq[i] : kEmpty;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mine += b + j * kGateThreads < c && (uint32_t)(e[j] >> 32) <= t;
+  }
   for (int o = 32; o >= 1; o >>= 1) mine += __shfl_xor(mine, o);
   if ((threadIdx.x & 63) == 0) atomicAdd(&tot, mine);
   __syncthreads();
@@ -4538,8 +4548,8 @@ int launch_overflow_gate(const uint64_t* cand, uint32_t* count, const uint64_t* 
     set_error("overflow gate: nq=%lld den=%lld", (long long)nq, (long long)den);
     return FX_EINVAL;
   }
-  hipLaunchKernelGGL(overflow_gate_kernel, dim3((unsigned)nq), dim3(256), 0, stream, cand, count,
-                     thr, cap, num, den);
+  hipLaunchKernelGGL(overflow_gate_kernel, dim3((unsigned)nq), dim3(kGateThreads), 0, stream, cand,
+                     count, thr, cap, num, den);
   return check_launch("overflow_gate_kernel");
 }
 

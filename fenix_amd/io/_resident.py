@@ -70,6 +70,19 @@ def combined(version: tuple, name: str, col: pa.ChunkedArray) -> pa.Array:
     return comb
 
 
+def null_count(version: tuple, name: str, col: pa.ChunkedArray) -> int:
+    """A column's null count, cached per file version (ChunkedArray.null_count
+    walks every chunk: ~0.1 ms per search over 10 000 1 000-row batches)."""
+    key = (version, name, "null_count")
+    with _lock:
+        hit = _COMBINED.get(key)
+    if hit is None:
+        hit = int(col.null_count)
+        with _lock:
+            _COMBINED[key] = hit
+    return hit
+
+
 def null_mask(version: tuple, name: str, col: pa.ChunkedArray) -> np.ndarray:
     """bool[rows]: the null slots of a column (cached per file version)."""
     key = (version, name, "null")

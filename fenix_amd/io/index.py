@@ -229,7 +229,7 @@ def _take_columns(data: pa.Table, cols: List[str], rows: np.ndarray, column: str
         col = data.column(c)
         if c == column:
             null = None
-            if col.null_count:
+            if (col.null_count if version is None else _resident.null_count(version, c, col)):
                 null = (_resident.null_mask(version, c, col) if version is not None
                         else _null_mask(col))[rows]
             arrays.append(_gather_vectors(shards, rows, col.type, null, values))
@@ -237,7 +237,8 @@ def _take_columns(data: pa.Table, cols: List[str], rows: np.ndarray, column: str
             arrays.append(_take_chunked(col, rows))
         else:
             arrays.append(_resident.combined(version, c, col).take(pa.array(rows)))
-    return pa.Table.from_arrays(arrays, schema=data.select(cols).schema)
+    return pa.Table.from_arrays(arrays, schema=pa.schema([data.schema.field(c) for c in cols],
+                                                         metadata=data.schema.metadata))
 
 
 _register_lock = threading.Lock()

@@ -99,6 +99,10 @@ int fx_device_count(int* out);
  *                            run the queries-in-registers kernel (except the
  *                            all-pass first sample); 0: the streamed-query-tile
  *                            kernel
+ *   "i8_sample_ratio"     8  int8 images: the final pass's sample F1 holds every
+ *                            r1-th tile (at least 2, at most cap / 4k)
+ *   "i8_grow_ratio"      16  int8 images: each sample before F1 is r2 times
+ *                            smaller than the next (at least 2, at most cap / 4k)
  *   "force_fallback"      0  1: every batched query is recomputed by the exact
  *                            single-query scan, as if its candidates overflowed
  *   "scan_interleave"    -1  -1: by row size; 0: one row range per workgroup;

@@ -1202,3 +1202,44 @@ def test_search_shards_one_merge_equals_per_shard(eng, metric, dtype):
     gd, gr = eng.search(shards, q, m, 100)
     # (global rows increase with the concatenated index: the same tie order)
     check_topk(gd.cpu().numpy(), gr.cpu().numpy(), od, glob[orow], allx, q.numpy(), metric)
+
+
+@pytest.mark.parametrize("metric", METRICS)
+@pytest.mark.parametrize("dtype,n,d,nq,k", [
+    (torch.float16, 400_000, 256, 1, 1000),   # one query, ~10^4-10^5 candidates
+    (torch.float32, 300_000, 128, 3, 600),
+    (torch.float16, 200_000, 1536, 5, 1000),  # configs[4]'s width
+])
+def test_int8_large_k_pruned_selects_bit_identical(eng, metric, dtype, n, d, nq, k):
+    """k >= 512 through the int8 image (option i8_max_k raised): every
+    select over the large candidate buffer first keeps the k smallest of each
+    16 K slice in parallel (select_kernel MODE 3, knn_batch.hip) and then
+    selects from those k-lists.  Results equal the exact scan bit for bit,
+    and through the overflow fallback (force_fallback: the final select
+    takes the fallback lists, never the pruned ones).  Reference: the
+    select_k_unstable of index.py:165-168 with an unbounded maxval."""
+    x = gpu_fill(eng, n, d, seed=71, dtype=dtype)
+    q = O.fill_normal(nq, d, seed=72)
+    q[0] = O.fill_normal(n, d, 71)[n // 3] if nq > 1 else q[0]  # a query near the corpus
+    m = _lib.METRICS[metric]
+    eng.clear_images()
+    with _lib.options(i8_max_k=1024, batch_min_queries=1):
+        assert _lib.filter_image_used(n, d, eng_dtype(dtype), nq, k, m)
+        fd, fr = gpu_search(eng, x, q, metric, k)
+        shard = Shard(x, 0)
+        st = eng.scan(shard, torch.as_tensor(q).to(eng.device), m, k)
+        counts, cap = eng.filter_counts(shard, nq, m, k, st)
+        with _lib.options(force_fallback=1):
+            gd, gr = gpu_search(eng, x, q, metric, k)
+    with _lib.options(batched=0):
+        sd, sr = gpu_search(eng, x, q, metric, k)
+    eng.clear_images()
+    assert cap > 2 * 16384  # the prune plan (select_prune_lists)
+    print(f"candidate counts {counts.tolist()} cap {cap}")
+    for dd, rr in ((fd, fr), (gd, gr)):
+        np.testing.assert_array_equal(rr, sr)
+        np.testing.assert_array_equal(dd.view(np.uint32), sd.view(np.uint32))
+
+
+def eng_dtype(dtype):
+    return _lib.DTYPE_F16 if dtype == torch.float16 else _lib.DTYPE_F32

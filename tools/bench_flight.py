@@ -16,8 +16,10 @@ into HBM and is reported separately.
 from __future__ import annotations
 
 import argparse
+import atexit
 import json
 import os
+import shutil
 import socket
 import subprocess
 import sys
@@ -37,6 +39,24 @@ def client(a) -> None:
 
     assert "torch" not in sys.modules
     f = fenix_amd.Flight(host="127.0.0.1", port=a.port)
+    if a.read_all:  # the reference client's last step: FlightStreamReader.read_all()
+        import pickle
+
+        import pyarrow.flight as fl
+
+        def search(target, source, column, metric, maxval):
+            cmd = {"coding": None, "source": source, "column": column, "metric": metric,
+                   "select": None, "filter": pickle.dumps(None), "maxval": maxval,
+                   "probes": None}
+            table = pa.table({"target": pa.array(target)})
+            w, r = f.conn.do_exchange(fl.FlightDescriptor.for_command(pickle.dumps(cmd)))
+            with w:
+                w.begin(table.schema)
+                w.write_table(table)
+                w.done_writing()
+                return r.read_all()
+
+        f = type("RefClient", (), {"search": staticmethod(search)})
     rs = np.random.RandomState(1)
     qs = rs.standard_normal((a.reps + 1, a.d)).astype(np.float16 if a.dtype == "f16" else np.float32)
     t0 = time.perf_counter()
@@ -74,6 +94,9 @@ def main() -> None:
     p.add_argument("--canned", action="store_true",
                    help="the server answers every search with the first search's result "
                         "table (no io.index.call): the Flight + gRPC floor above the engine")
+    p.add_argument("--read-all", action="store_true",
+                   help="client: read the reply with FlightStreamReader.read_all() as the "
+                        "reference's Flight.search does (flight.py:288)")
     p.add_argument("--client", action="store_true")
     p.add_argument("--port", type=int, default=0)
     p.add_argument("--source", default="bench/table", help="client: the table to search")
@@ -108,6 +131,7 @@ def main() -> None:
                                   names=["id", "vector"])
 
     root = tempfile.mkdtemp(prefix="fenix_bench_", dir=a.root or None)
+    atexit.register(shutil.rmtree, root, True)  # (a 10M x 768 source is 30 GB of disk)
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -135,7 +159,7 @@ def main() -> None:
         _index.call = canned
     cmd = [sys.executable, os.path.abspath(__file__), "--client", "--port", str(port),
            "--d", str(a.d), "--k", str(a.k), "--metric", a.metric, "--dtype", a.dtype,
-           "--reps", str(a.reps)]
+           "--reps", str(a.reps)] + (["--read-all"] if a.read_all else [])
     t_all = time.perf_counter()
     procs = [subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
              for _ in range(a.clients)]
@@ -167,6 +191,8 @@ def main() -> None:
             np.sum(r["lat_ms"]) / 1e3 / a.clients for r in results) if a.clients > 1 else None,
         "wall_s_incl_client_start": wall,
         "canned_reply": a.canned,
+        "client_read": "FlightStreamReader.read_all (the reference client)" if a.read_all
+                       else "reader.to_reader().read_all() (fenix_amd.Flight.search)",
         "coalesce": coalesce.enabled(),
         "coalesced": coalesce.describe(coalesce.default()),
     }), flush=True)

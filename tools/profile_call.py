@@ -14,11 +14,13 @@ measure what that does to the next call.
 from __future__ import annotations
 
 import argparse
+import atexit
 import collections
 import cProfile
 import json
 import os
 import pstats
+import shutil
 import sys
 import tempfile
 import time
@@ -56,6 +58,7 @@ def main() -> None:
     tdt = torch.float16 if a.dtype == "f16" else torch.float32
     vt = pa.list_(pa.float16() if a.dtype == "f16" else pa.float32(), a.d)
     root = tempfile.mkdtemp(prefix="fenix_prof_")
+    atexit.register(shutil.rmtree, root, True)  # (a 10M x 768 source is 30 GB of disk)
     dev = torch.empty((100_000, a.d), dtype=tdt, device=eng.device)
 
     def batches():
@@ -81,7 +84,10 @@ def main() -> None:
     # phase clocks: wrap the functions io.index.call goes through
     phases = collections.defaultdict(list)
 
-    def clocked(mod, name):
+    # and a timeline of each call: (function, start, end) in us from the call's start
+    events: list = []
+
+    def clocked(mod, name, phase=True):
         fn = getattr(mod, name)
 
         def wrapper(*args, **kw):
@@ -89,7 +95,10 @@ def main() -> None:
             try:
                 return fn(*args, **kw)
             finally:
-                phases[name].append((time.perf_counter() - t) * 1e3)
+                e = time.perf_counter()
+                if phase:
+                    phases[name].append((e - t) * 1e3)
+                events.append((name, t, e))
 
         setattr(mod, name, wrapper)
         return fn
@@ -99,15 +108,30 @@ def main() -> None:
                       (index, "_take_columns"), (index, "_gather_vectors"),
                       (index, "_take_chunked")):
         clocked(mod, name)
+    from fenix_amd import coalesce, engine
+
+    for mod, name in ((engine, "_search_all"), (engine.Engine, "search"),
+                      (engine.Engine, "search_shard"), (engine.Engine, "filter_image"),
+                      (engine, "gather_rows"), (engine, "_to_host"), (engine, "check_rows"),
+                      (coalesce.Coalescer, "search")):
+        clocked(mod, name, phase=False)
+    timeline = []
 
     def run(qi: int) -> float:
+        events.clear()
         t = time.perf_counter()
         r = index.call(root, None, "p/t", "vector", target=qs[qi], metric=a.metric, maxval=a.k)
-        ms = (time.perf_counter() - t) * 1e3
+        e = time.perf_counter()
+        ms = (e - t) * 1e3
         assert r.num_rows == a.k
+        timeline[:] = [("index.call", t, e)] + sorted(events, key=lambda v: v[1])
         return ms
 
     ts = [run(1 + i) for i in range(a.reps)]
+    t0 = timeline[0][1]
+    print("timeline of the last call (us from its start: start, end, duration):")
+    for name, s_, e_ in timeline:
+        print(f"  {(s_ - t0) * 1e6:8.1f} {(e_ - t0) * 1e6:8.1f} {(e_ - s_) * 1e6:8.1f}  {name}")
     print("index.call ms: median %.3f min %.3f max %.3f" % (np.median(ts), min(ts), max(ts)),
           flush=True)
     breakdown = {k: float(np.median(v)) for k, v in phases.items()}
@@ -128,6 +152,7 @@ def main() -> None:
         run(1 + i)
     pr.disable()
     pstats.Stats(pr).sort_stats("cumulative").print_stats(35)
+    pstats.Stats(pr).sort_stats("tottime").print_stats(40)
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"workload": f"{a.n}x{a.d} {a.dtype} {a.metric} k={a.k}, "

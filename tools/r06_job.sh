@@ -32,6 +32,19 @@ for step in "$@"; do
         --direct --reps 60 --canned ;;
     tests) run tests 900 python -u -m pytest $TESTS -m gpu -x -v -p no:cacheprovider --timeout 300 \
         --timeout-method thread ;;
+    ksweep) run ksweep 900 python -u tools/k1000_sweep.py --queries 20 --opt i8_max_k=1024 \
+        --json gpurun_out/r06/k1000_sweep.json ;;
+    ktrace) run ktrace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r06/ktrace -o run \
+        --output-format csv -- python3 -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
+        --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024 --steps 5 --warmup 1
+      python tools/timeline.py gpurun_out/r06/ktrace/run_kernel_trace.csv qprep8 \
+        > gpurun_out/r06/ktrace_timeline.txt ;;
+    ctrace) run ctrace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r06/ctrace -o run \
+        --output-format csv -- python3 -u bench.py --no-cpu-baseline --no-batch-leg --steps 5 --warmup 1
+      python tools/timeline.py gpurun_out/r06/ctrace/run_kernel_trace.csv qprep8 \
+        > gpurun_out/r06/ctrace_timeline.txt ;;
+    flightr) run flightr 600 python -u tools/bench_flight.py --n 10000000 --d 768 --k 100 --metric l2 \
+        --direct --reps 60 --read-all ;;
     flight0) run flight0 300 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 --reps 60 ;;
     k1000) run k1000a 300 python -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
         --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024
