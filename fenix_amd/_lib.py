@@ -96,7 +96,7 @@ SYMBOLS = (
 # test switches
 OPTIONS = ("batched", "batch_min_queries", "batch_cap", "batch_sample_ratio", "force_fallback",
            "scan_interleave", "q8_dma", "filter_image", "batch_ub_test", "single_query_image",
-           "i8_max_k", "img6", "img8")
+           "i8_max_k", "img6", "img8", "i8_sample_ratio", "i8_grow_ratio", "select_prune")
 
 _lock = threading.Lock()
 _lib = None

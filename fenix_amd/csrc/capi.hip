@@ -41,9 +41,10 @@ static std::mutex g_mu;
 static const char* const kOptNames[kOptCount] = {
     "batched", "batch_min_queries", "batch_cap", "batch_sample_ratio",
     "force_fallback", "scan_interleave", "q8_dma", "filter_image", "batch_ub_test",
-    "single_query_image", "i8_max_k", "img6", "img8", "i8_sample_ratio", "i8_grow_ratio"};
+    "single_query_image", "i8_max_k", "img6", "img8", "i8_sample_ratio", "i8_grow_ratio",
+    "select_prune"};
 static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}, {8}, {1}, {1},
-                                                 {256}, {1}, {1}, {8}, {16}};
+                                                 {256}, {1}, {1}, {8}, {16}, {1}};
 
 int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
 

@@ -33,6 +33,7 @@ enum Option : int {
   kOptImg8,         // int8 images: queries-in-registers kernel for > 128 queries, d <= 768 (0: off)
   kOptI8SampleRatio,  // int8 images: F1 holds every r1-th tile (filter_phases_i8)
   kOptI8GrowRatio,    // int8 images: the samples before F1 shrink by r2 each
+  kOptSelectPrune,    // int8 images: 1: selects at k >= 512 prune first; 2: any k; 0: never
   kOptCount
 };
 int64_t option(Option o);

@@ -784,7 +784,8 @@ __global__ void __launch_bounds__(kSelectThreads)
 // plans at k ~ 1 000: ~100 K candidates per query).  k-lists per query, 0 = off.
 constexpr int kPruneMinK = 512;
 int select_prune_lists(int64_t k, int64_t cap) {
-  if (k < kPruneMinK || cap <= 2 * (int64_t)kSelectEntries) return 0;
+  const int64_t o = option(kOptSelectPrune);
+  if (o == 0 || (o == 1 && k < kPruneMinK) || cap <= 2 * (int64_t)kSelectEntries) return 0;
   return (int)((cap + kSelectEntries - 1) / kSelectEntries);
 }
 

@@ -103,6 +103,9 @@ int fx_device_count(int* out);
  *                            r1-th tile (at least 2, at most cap / 4k)
  *   "i8_grow_ratio"      16  int8 images: each sample before F1 is r2 times
  *                            smaller than the next (at least 2, at most cap / 4k)
+ *   "select_prune"        1  int8 images: the selects over the candidate buffer
+ *                            first keep the k smallest of each 16 K slice in
+ *                            parallel when k >= 512 (2: at any k; 0: never)
  *   "force_fallback"      0  1: every batched query is recomputed by the exact
  *                            single-query scan, as if its candidates overflowed
  *   "scan_interleave"    -1  -1: by row size; 0: one row range per workgroup;

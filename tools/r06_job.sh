@@ -21,6 +21,7 @@ run() {
   [ $rc -eq 0 ] || exit $rc
 }
 TESTS=${TESTS:-tests}
+K4="--dtype f16 --d 1536 --rows 6250000 --k 1000 --metric inner_product --no-batch-leg --opt i8_max_k=1024"
 for step in "$@"; do
   case $step in
     bench) run bench 300 python -u bench.py ;;
@@ -45,6 +46,15 @@ for step in "$@"; do
         > gpurun_out/r06/ctrace_timeline.txt ;;
     flightr) run flightr 600 python -u tools/bench_flight.py --n 10000000 --d 768 --k 100 --metric l2 \
         --direct --reps 60 --read-all ;;
+    rsweep1) run rsweep1 900 python -u tools/sweep.py --reps 2 --steps 20 --warmup 3 \
+        --out gpurun_out/r06/ratio_sweep_cfg1.jsonl -- "--no-batch-leg" \
+        "--no-batch-leg --opt i8_grow_ratio=32 --opt select_prune=2" \
+        "--no-batch-leg --opt i8_grow_ratio=20 --opt select_prune=2" \
+        "--no-batch-leg --opt select_prune=2" "--no-batch-leg --opt i8_sample_ratio=12" ;;
+    rsweep4) run rsweep4 900 python -u tools/sweep.py --reps 1 --steps 20 --warmup 3 \
+        --out gpurun_out/r06/ratio_sweep_k1000.jsonl -- \
+        "$K4 --opt i8_grow_ratio=16" "$K4 --opt i8_grow_ratio=8" "$K4 --opt i8_grow_ratio=32" \
+        "$K4 --opt i8_sample_ratio=4" "$K4 --opt i8_sample_ratio=16" "$K4 --opt select_prune=0" ;;
     flight0) run flight0 300 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 --reps 60 ;;
     k1000) run k1000a 300 python -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
         --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024
