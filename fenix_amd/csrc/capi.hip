@@ -695,9 +695,10 @@ static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, cons
   // the exact k-th of the k best upper bounds in `keys` -> thr (one fused
   // launch when the buffer fits one workgroup's LDS)
   uint64_t* prune = reinterpret_cast<uint64_t*>(w + b.off_prune);
+  int64_t* topr = reinterpret_cast<int64_t*>(w + b.off_topr);
   auto exact_threshold = [&](const uint64_t* keys, bool zero) {
     return launch_exact_threshold(X, dtype, n, (int)d, row_base, Q, qnorm, nq, keys, b.cap, count,
-                                  zero, (int)k, metric, thr, st, prune);
+                                  zero, (int)k, metric, thr, st, prune, topr);
   };
   const int m = b.nphases;
   for (int ph = 0; ph + 2 < m; ++ph) {  // sampling phases: thresholds only

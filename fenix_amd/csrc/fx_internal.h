@@ -163,7 +163,8 @@ size_t select_prune_bytes(int64_t nq, int64_t k, int64_t cap);
 int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t row_base,
                            const float* Q, const float* qnorm, int64_t nq, const uint64_t* keys,
                            int64_t cap, uint32_t* count, bool zero_count, int k, int metric,
-                           uint64_t* thr, hipStream_t stream, uint64_t* prune = nullptr);
+                           uint64_t* thr, hipStream_t stream, uint64_t* prune = nullptr,
+                           int64_t* topr = nullptr);
 // thr[q] = min(thr[q], the k-th smallest of the query's first count[q] keys)
 // when it has at least k (run_merge's threshold-only level, any cap)
 int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint32_t* count,

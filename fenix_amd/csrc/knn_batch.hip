@@ -673,7 +673,11 @@ __global__ void __launch_bounds__(kSelectThreads)
   }
   __syncthreads();
   if (zero_count && tid == 0) count[q * kCountStride] = 0u;
-  if (MODE != 1 && m < k) return;  // (uniform) fewer than k candidates: no threshold
+  if (MODE != 1 && m < k) {  // (uniform) fewer than k candidates: no threshold
+    if (MODE == 0 && out_row != nullptr)  // (rows out: none, the query keeps its threshold)
+      for (int i = tid; i < k; i += kSelectThreads) out_row[q * k + i] = -1;
+    return;
+  }
   if (pre != nullptr && !use_alt) {  // the pruned k-lists of the same entries (MODE 3)
     src = pre + q * pre_p * (int64_t)k;
     m = (m + pre_s - 1) / pre_s * k;
@@ -731,6 +735,13 @@ __global__ void __launch_bounds__(kSelectThreads)
     __syncthreads();
     if (tid == 0 && ms->shmax < thr[q]) thr[q] = ms->shmax;
   } else if constexpr (MODE == 0) {
+    if (out_row != nullptr) {  // rows out: rescored by the whole chip (launch_exact_kth)
+      for (int j = tid; j < k; j += kSelectThreads) {
+        const uint64_t e = j < nres ? res[j] : kEmpty;
+        out_row[q * k + j] = e == kEmpty ? -1 : (int64_t)(e & 0xffffffffull);
+      }
+      return;
+    }
     if (tid == 0) ms->shmax = 0ull;
     __syncthreads();
     const int grp = tid >> 4, jl = tid & 15;
@@ -861,10 +872,25 @@ static int launch_select_t(const T* X, int64_t n, int d, int64_t row_base, const
 int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t row_base,
                            const float* Q, const float* qnorm, int64_t nq, const uint64_t* keys,
                            int64_t cap, uint32_t* count, bool zero_count, int k, int metric,
-                           uint64_t* thr, hipStream_t stream, uint64_t* prune) {
+                           uint64_t* thr, hipStream_t stream, uint64_t* prune, int64_t* topr) {
   if (k > kSelectMaxK || k > cap) {
     set_error("exact threshold: k %d beyond cap %lld", k, (long long)cap);
     return FX_EUNSUPPORTED;
+  }
+  if (prune != nullptr && topr != nullptr && select_prune_lists(k, cap) > 0) {
+    // large k: the pruned select writes the k rows, the chip rescores them
+    // (one workgroup rescoring 1 000 rows of 3 KB took ~40 us of its time)
+    int rc = dtype == FX_DTYPE_F16
+                 ? launch_select_t<_Float16, 0>(reinterpret_cast<const _Float16*>(X), n, d,
+                                                row_base, Q, qnorm, nq, keys, cap, count,
+                                                zero_count ? 1 : 0, k, metric, thr, nullptr, topr,
+                                                nullptr, 0, 0, stream, prune)
+                 : launch_select_t<float, 0>(reinterpret_cast<const float*>(X), n, d, row_base, Q,
+                                             qnorm, nq, keys, cap, count, zero_count ? 1 : 0, k,
+                                             metric, thr, nullptr, topr, nullptr, 0, 0, stream,
+                                             prune);
+    if (rc) return rc;
+    return launch_exact_kth(X, dtype, n, d, row_base, Q, qnorm, nq, k, topr, metric, thr, stream);
   }
   if (dtype == FX_DTYPE_F16)
     return launch_select_t<_Float16, 0>(reinterpret_cast<const _Float16*>(X), n, d, row_base, Q,
