@@ -861,19 +861,22 @@ __device__ __forceinline__ void filter_tiles(const FilterArgs& a, unsigned char*
 // candidate buffer: one global atomic per query reserves the slots.  seg =
 // [fBQ counters][fBQ x SEG entries {lb key, ub key, row}]; called by every
 // thread after the last tile (ends with the counters reused as bases).
+// segcap: entries per query (SEG, or more when the slice has fewer live
+// queries: i8_epilogue's segcap), fBQ * SEG entries in all.
 template <int SEG, int NT = fThreads>
 __device__ __forceinline__ void filter_flush_segments(uint32_t* seg, uint32_t* base,
-                                                      const FilterArgs& a, int64_t q0, int tid) {
+                                                      const FilterArgs& a, int64_t q0, int tid,
+                                                      int segcap = SEG) {
   __syncthreads();
   for (int q = tid; q < fBQ; q += NT) {
-    const uint32_t n = seg[q] < (uint32_t)SEG ? seg[q] : (uint32_t)SEG;
+    const uint32_t n = seg[q] < (uint32_t)segcap ? seg[q] : (uint32_t)segcap;
     seg[q] = n;
     base[q] = n != 0u && q0 + q < a.nq ? atomicAdd(&a.count[(q0 + q) * kCountStride], n) : 0u;
   }
   __syncthreads();
   for (int i = tid; i < fBQ * SEG; i += NT) {
-    const int q = i / SEG, j = i % SEG;
-    if ((uint32_t)j >= seg[q]) continue;
+    const int q = i / segcap, j = i % segcap;
+    if (q >= fBQ || (uint32_t)j >= seg[q]) continue;
     const uint32_t p = base[q] + (uint32_t)j;
     if (p >= (uint32_t)a.cap) continue;
     const uint32_t* e = seg + fBQ + 3 * i;
@@ -1507,8 +1510,8 @@ __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const fl
                                             const uint32_t* rrow, const uint32_t* flags,
                                             const f32x4* qtab, const f32x4* qinf,
                                             const FilterArgs& a, int64_t q0, int wid, int h,
-                                            int l32, uint32_t* seg, int diag) {
-  constexpr int SEG = FX_I3_SEG;
+                                            int l32, uint32_t* seg, int diag,
+                                            int segcap = FX_I3_SEG) {
   const int lr0 = wid * 32 + 4 * h;
   const uint32_t fmask = flags[wid * 2 + h], smask = flags[16 + wid * 2 + h];
   // row groups g of 4 rows outside (their values read once from LDS), query
@@ -1555,8 +1558,11 @@ __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const fl
     pm[u] = (diag & 1) ? 0u : (~fail[u] | force) & ~smask & 0xffffu;
     if (q0 + u * 32 + l32 >= a.nq) pm[u] = 0u;
   }
-  if (a.all_pass) {  // no threshold yet (first phase): every live pair, slots reserved
-                     // per lane and query, accumulators indexed statically
+  if (a.all_pass && segcap <= FX_I3_SEG) {  // no threshold yet (first phase): every live
+                     // pair, slots reserved per lane and query, accumulators indexed
+                     // statically (a slice of few live queries appends through its
+                     // segments below instead: one query's whole sample otherwise
+                     // meets in one global counter, ~3 K atomics)
     static_for<kI2QT>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
       const uint32_t bits = pm[u];
@@ -1621,8 +1627,8 @@ __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const fl
       float lb, ub;
       i8_bounds<METRIC>(x, rinfo[lr], rterm[lr], rext[lr], qrec, a.d, lb, ub);
       const uint32_t grow = rrow[lr];
-      if (p < (uint32_t)SEG) {
-        lds_write3_u32(seg + fBQ + 3 * (qi * SEG + p), order_key(lb), order_key(ub), grow);
+      if (p < (uint32_t)segcap) {
+        lds_write3_u32(seg + fBQ + 3 * (qi * segcap + p), order_key(lb), order_key(ub), grow);
       } else {  // rare: past the segment, global slots for the lane's remaining passes
         if (gp == ~0u) gp = atomicAdd(&a.count[gq * kCountStride], (uint32_t)__popc(rest));
         if (gp < (uint32_t)a.cap) {
@@ -2672,6 +2678,12 @@ __global__ void __launch_bounds__(kI6Threads, 1) filter_img6_kernel(FilterArgs a
   }
   i8_query_table<METRIC>(a, q0, sh->qtab, sh->qinf, tid, kI6Threads);
   for (int q = tid; q < fBQ; q += kI6Threads) sh->seg[q] = 0u;
+  // the slice's live queries share all fBQ * SEG segment entries (one query:
+  // 1 536 instead of 24, so a k = 1 000 search's ~200 appends per workgroup
+  // and phase stay in LDS instead of each lane taking a slot from the one
+  // global counter of the query: F1 429 us at 6.25M x 1536)
+  const int64_t nlive = a.nq - q0 < fBQ ? a.nq - q0 : fBQ;
+  const int segcap = (fBQ * SEG) / (int)(nlive > 0 ? nlive : 1);
   {  // the slice: chunk c of query Q at (c * 128 + Q) * 64, piece p at (p ^ ((Q >> 2) & 3)) * 16
     // (kI6SliceBatch loads in flight per thread before their stores: one
     // load, wait, store per iteration cost ~1.5 us each, ~18 us per launch)
@@ -2820,11 +2832,11 @@ __global__ void __launch_bounds__(kI6Threads, 1) filter_img6_kernel(FilterArgs a
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (!(diag & 2))
       i8_epilogue<METRIC>(acc, sh->rinfo, sh->rterm, sh->rext, sh->rrow, sh->rflags, sh->qtab,
-                          sh->qinf, a, q0, wid, h, l32, sh->seg, diag);
+                          sh->qinf, a, q0, wid, h, l32, sh->seg, diag, segcap);
     xr = xn;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  filter_flush_segments<SEG, kI6Threads>(sh->seg, sh->segbase, a, q0, tid);
+  filter_flush_segments<SEG, kI6Threads>(sh->seg, sh->segbase, a, q0, tid, segcap);
 }
 
 int launch_img6(const FilterArgs& a, int metric, hipStream_t stream) {

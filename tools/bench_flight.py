@@ -44,12 +44,14 @@ def client(a) -> None:
 
         import pyarrow.flight as fl
 
+        conn = f.conn
+
         def search(target, source, column, metric, maxval):
             cmd = {"coding": None, "source": source, "column": column, "metric": metric,
                    "select": None, "filter": pickle.dumps(None), "maxval": maxval,
                    "probes": None}
             table = pa.table({"target": pa.array(target)})
-            w, r = f.conn.do_exchange(fl.FlightDescriptor.for_command(pickle.dumps(cmd)))
+            w, r = conn.do_exchange(fl.FlightDescriptor.for_command(pickle.dumps(cmd)))
             with w:
                 w.begin(table.schema)
                 w.write_table(table)
