@@ -44,7 +44,7 @@ static const char* const kOptNames[kOptCount] = {
     "single_query_image", "i8_max_k", "img6", "img8", "i8_sample_ratio", "i8_grow_ratio",
     "select_prune"};
 static std::atomic<int64_t> g_opts[kOptCount] = {{1}, {2}, {0}, {0}, {0}, {-1}, {1}, {8}, {1}, {1},
-                                                 {256}, {1}, {1}, {8}, {16}, {1}};
+                                                 {1024}, {1}, {1}, {8}, {16}, {1}};
 
 int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
 
@@ -217,10 +217,14 @@ static bool use_filter() { return diag_env("FX_BATCH_FILTER", 1) != 0; }
 // points, option "single_query_image"): 10M x 768 1.41 vs 4.34 ms; the
 // filter path's fixed cost (~0.25 ms of small launches) loses below ~2.4 GB
 static constexpr int64_t kSingleImageMinBytes = (int64_t)4 << 30;
-// The int8 image's bounds are wide: with k = 1 000 the final phase of a
-// 6.25M x 1536 fp16 IP search appended more than its 64 K candidate slots for
-// most queries (Flight, profiles/r03_f16_int8_image.log), and each overflow
-// costs a full rescan.  Int8 images serve k <= option "i8_max_k" only.
+// Int8 images serve k <= option "i8_max_k" (1 024 = kMaxK, every k the
+// filter plans).  Round 3's 64 K slots overflowed at k = 1 000 (6.25M x 1536
+// fp16 IP, profiles/r03_f16_int8_image.log); with the 4x buffer (256 K slots
+// at k = 1 000), the pruned selects (select_kernel MODE 3) and the shared LDS
+// append segments, 60 single queries (normal, near, clustered corpus) kept
+// 94-122 K candidates, none overflowed, 1.67 vs 2.84 ms for the exact scan,
+// bit-identical (profiles/r06_k1000_sweep*.json); batches at k 300-1 000 are
+// faster too (profiles/r06_kbatch_i8_max_k.jsonl).
 static int64_t i8_max_k() { return option(kOptI8MaxK); }
 
 static bool use_batched(int64_t nq, int dtype, int metric, int64_t d, bool aligned, int64_t n,

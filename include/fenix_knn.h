@@ -87,7 +87,7 @@ int fx_device_count(int* out);
  *                            bound reaches the threshold (0: lower bound)
  *   "single_query_image"  1  0: single queries keep the exact scan even when
  *                            an int8 filter image is supplied
- *   "i8_max_k"          256  largest k an int8 filter image serves (larger k:
+ *   "i8_max_k"         1024  largest k an int8 filter image serves (larger k:
  *                            the fp16 image / f32 rows, or the exact scan);
  *                            at most 2048 (FX_EINVAL above)
  *   "img6"                1  1: int8-image batches of <= 128 queries (single

@@ -749,9 +749,9 @@ def test_filter_image_bit_identical(eng, metric, n, d, nq, k, bits):
     q[min(1, nq - 1)] = xh[7] if nq > 1 else q[0]
     eng.clear_images()
     with _lib.options(filter_image=bits):
-        # (int8 images serve k <= 256: capi.hip kI8MaxK)
+        # (int8 images serve k <= option i8_max_k, 1 024 by default)
         used = _lib.filter_image_used(n, d, _lib.DTYPE_F32, nq, k, _lib.METRICS[metric])
-        assert used == (bits == 16 or k <= 256)
+        assert used == (bits == 16 or k <= _lib.get_option("i8_max_k"))
         id_, ir = gpu_search(eng, x, q, metric, k)  # MFMA-fragment-order image
     if used:
         assert eng._images[id(x)][0][3] == bits  # the image path ran
@@ -803,9 +803,14 @@ def test_single_query_through_filter_image(eng, metric, bits):
         assert not _lib.filter_image_used(*big, _lib.DTYPE_F32, 1, k, m)
     # an fp16 column takes the int8 image too (>= 4 GiB of fp16 rows), never an fp16 image
     assert _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, k, m)
-    # k > 256: int8 bounds would overflow the candidate buffer (kI8MaxK)
-    assert not _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, 1000, m)
-    assert not _lib.filter_image_used(*big, _lib.DTYPE_F32, 1, 1000, m)
+    # k = 1 000 (configs[4]) takes the int8 image too (i8_max_k 1 024,
+    # profiles/r06_k1000_sweep.json); k above i8_max_k does not
+    assert _lib.get_option("i8_max_k") == 1024
+    assert _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, 1000, m)
+    assert _lib.filter_image_used(*big, _lib.DTYPE_F32, 1, 1000, m)
+    with _lib.options(i8_max_k=256):
+        assert not _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, 1000, m)
+        assert not _lib.filter_image_used(*big, _lib.DTYPE_F32, 1, 1000, m)
     with _lib.options(filter_image=16):
         assert not _lib.filter_image_used(*big, _lib.DTYPE_F16, 1, k, m)
 

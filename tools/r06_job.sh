@@ -55,6 +55,19 @@ for step in "$@"; do
         --out gpurun_out/r06/ratio_sweep_k1000.jsonl -- \
         "$K4 --opt i8_grow_ratio=16" "$K4 --opt i8_grow_ratio=8" "$K4 --opt i8_grow_ratio=32" \
         "$K4 --opt i8_sample_ratio=4" "$K4 --opt i8_sample_ratio=16" "$K4 --opt select_prune=0" ;;
+    kbatch) K16="--dtype f16 --d 1536 --rows 6250000 --metric inner_product --no-batch-leg --k 1000"
+      run kbatch 1100 python -u tools/sweep.py --reps 1 --steps 10 --warmup 2 \
+        --out gpurun_out/r06/kbatch.jsonl -- \
+        "$K16 --nq 16 --opt i8_max_k=256" "$K16 --nq 16 --opt i8_max_k=1024" \
+        "$K16 --nq 256 --opt i8_max_k=256" "$K16 --nq 256 --opt i8_max_k=1024" \
+        "--no-batch-leg --k 1000 --nq 16 --opt i8_max_k=256" "--no-batch-leg --k 1000 --nq 16 --opt i8_max_k=1024" \
+        "--no-batch-leg --k 300 --nq 256 --metric cosine --opt i8_max_k=256" \
+        "--no-batch-leg --k 300 --nq 256 --metric cosine --opt i8_max_k=1024" ;;
+    kclust) run kclust 900 python -u tools/k1000_sweep.py --queries 10 --cluster 1000 --opt i8_max_k=1024 \
+        --json gpurun_out/r06/k1000_sweep_cluster.json ;;
+    abseg) run abseg 1100 python -u tools/sweep.py --libs new,old --reps 2 --steps 20 --warmup 3 \
+        --out gpurun_out/r06/abseg.jsonl -- "--no-batch-leg" "--no-batch-leg --nq 256 --metric cosine" \
+        "$K4" ;;
     flight0) run flight0 300 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 --reps 60 ;;
     k1000) run k1000a 300 python -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
         --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024
