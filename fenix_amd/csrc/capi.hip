@@ -700,9 +700,11 @@ static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, cons
   // launch when the buffer fits one workgroup's LDS)
   uint64_t* prune = reinterpret_cast<uint64_t*>(w + b.off_prune);
   int64_t* topr = reinterpret_cast<int64_t*>(w + b.off_topr);
-  auto exact_threshold = [&](const uint64_t* keys, bool zero) {
+  auto exact_threshold = [&](const uint64_t* keys, bool zero, const uint64_t* gate = nullptr,
+                             int64_t gate_num = 0, int64_t gate_den = 1) {
     return launch_exact_threshold(X, dtype, n, (int)d, row_base, Q, qnorm, nq, keys, b.cap, count,
-                                  zero, (int)k, metric, thr, st, prune, topr);
+                                  zero, (int)k, metric, thr, st, prune, topr, gate, gate_num,
+                                  gate_den);
   };
   const int m = b.nphases;
   for (int ph = 0; ph + 2 < m; ++ph) {  // sampling phases: thresholds only
@@ -724,12 +726,12 @@ static int filter_phases_i8(const BatchLayout& b, const void* X, int dtype, cons
   rc = launch_filter(f1, metric, st);
   if (rc) return rc;
   if (m >= 2) {
-    rc = exact_threshold(cand_ub, false);
-    if (rc) return rc;
     const int64_t t1 = b.num[m - 2], t2 = b.tiles - t1;
+    // F1's threshold, then (t2 > 0) the overflow gate on it (launch_overflow_gate's
+    // prediction, run by the select's own workgroups)
+    rc = t2 > 0 ? exact_threshold(cand_ub, false, cand, t2, t1) : exact_threshold(cand_ub, false);
+    if (rc) return rc;
     if (t2 > 0) {
-      rc = launch_overflow_gate(cand, count, thr, nq, (int)b.cap, t2, t1, st);
-      if (rc) return rc;
       // F2: the tiles after F1's prefix
       FilterArgs f2 = args(m - 1);
       f2.tile_start = t1;

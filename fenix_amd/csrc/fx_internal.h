@@ -164,7 +164,11 @@ int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t r
                            const float* Q, const float* qnorm, int64_t nq, const uint64_t* keys,
                            int64_t cap, uint32_t* count, bool zero_count, int k, int metric,
                            uint64_t* thr, hipStream_t stream, uint64_t* prune = nullptr,
-                           int64_t* topr = nullptr);
+                           int64_t* topr = nullptr, const uint64_t* gate_cand = nullptr,
+                           int64_t gate_num = 0, int64_t gate_den = 1);
+// (gate_cand: launch_overflow_gate(gate_cand, count, thr, nq, cap, gate_num,
+// gate_den) follows on the new thresholds, fused into the select's workgroups
+// when the select computes them itself)
 // thr[q] = min(thr[q], the k-th smallest of the query's first count[q] keys)
 // when it has at least k (run_merge's threshold-only level, any cap)
 int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint32_t* count,

@@ -612,6 +612,43 @@ int launch_exact_kth(const void* X, int dtype, int64_t n, int d, int64_t row_bas
 #define FX_SELECT_THREADS 1024
 #endif
 constexpr int kSelectThreads = FX_SELECT_THREADS;
+
+// overflow_gate_kernel's arithmetic (knn_filter.hip, launch_overflow_gate) in
+// the exact-threshold select's own workgroup, on the threshold it just set:
+// the query's c appended lb composites of cand under thr, scaled by num / den
+// and added to c; a query predicted past cap gets count = cap + 1.  Saves the
+// gate's own launch (~5 us per search, profiles/r06_cfg1_img8_timeline.txt).
+// Every thread calls it (barriers inside).
+__device__ __forceinline__ void select_gate(const uint64_t* __restrict__ cand,
+                                            uint32_t* __restrict__ count, int64_t q, uint32_t c,
+                                            int64_t cap, uint64_t thrq, int64_t num, int64_t den,
+                                            MergeShared* ms) {
+  if (c > (uint32_t)cap) return;  // (uniform; already overflowing: recomputed anyway)
+  const int tid = threadIdx.x;
+  if (tid == 0) ms->ctr_eq = 0u;
+  __syncthreads();
+  const uint32_t t = (uint32_t)(thrq >> 32);
+  const uint64_t* cq = cand + q * cap;
+  uint32_t mine = 0u;
+  for (uint32_t b = tid; b < c; b += kSelectThreads * 8) {
+    uint64_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = b + j * kSelectThreads;
+      e[j] = i < c ? cq[i] : kEmpty;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mine += b + j * kSelectThreads < c && (uint32_t)(e[j] >> 32) <= t;
+  }
+  for (int o = 32; o >= 1; o >>= 1) mine += __shfl_xor(mine, o);
+  if ((tid & 63) == 0) atomicAdd(&ms->ctr_eq, mine);
+  __syncthreads();
+  if (tid == 0) {
+    const uint64_t predicted =
+        (uint64_t)c + ((uint64_t)ms->ctr_eq * (uint64_t)num + (uint64_t)den - 1) / (uint64_t)den;
+    if (predicted > (uint64_t)cap) count[q * kCountStride] = (uint32_t)cap + 1u;
+  }
+}
 constexpr int kSelectEntries = 16384;  // LDS chunk (128 KB)
 template <typename T, int METRIC, int MODE>
 __global__ void __launch_bounds__(kSelectThreads)
@@ -621,7 +658,8 @@ __global__ void __launch_bounds__(kSelectThreads)
                   int zero_count, int k, int P2, uint64_t* __restrict__ thr,
                   float* __restrict__ out_dist, int64_t* __restrict__ out_row,
                   const uint64_t* __restrict__ alt, int64_t alt_m, int64_t alt_gate,
-                  uint64_t* __restrict__ pre, int pre_p, int64_t pre_s) {
+                  uint64_t* __restrict__ pre, int pre_p, int64_t pre_s,
+                  const uint64_t* __restrict__ gate_cand, int64_t gate_num, int64_t gate_den) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   MergeShared* ms = reinterpret_cast<MergeShared*>(smem);
   uint64_t* res = reinterpret_cast<uint64_t*>(smem + sizeof(MergeShared));
@@ -676,6 +714,8 @@ __global__ void __launch_bounds__(kSelectThreads)
   if (MODE != 1 && m < k) {  // (uniform) fewer than k candidates: no threshold
     if (MODE == 0 && out_row != nullptr)  // (rows out: none, the query keeps its threshold)
       for (int i = tid; i < k; i += kSelectThreads) out_row[q * k + i] = -1;
+    if (MODE == 0 && out_row == nullptr && gate_cand != nullptr)
+      select_gate(gate_cand, count, q, c, cap, thr[q], gate_num, gate_den, ms);
     return;
   }
   if (pre != nullptr && !use_alt) {  // the pruned k-lists of the same entries (MODE 3)
@@ -763,7 +803,49 @@ __global__ void __launch_bounds__(kSelectThreads)
     mx = wave_max_u64(mx);
     if (lane == 0) atomicMax(&ms->shmax, (unsigned long long)mx);
     __syncthreads();
-    if (tid == 0 && ms->shmax < thr[q]) thr[q] = ms->shmax;
+    if (tid == 0) {
+      const uint64_t old = thr[q];
+      const uint64_t nt = ms->shmax < old ? (uint64_t)ms->shmax : old;
+      thr[q] = nt;
+      ms->shmax = nt;  // (the gate's threshold)
+    }
+    if (gate_cand != nullptr) {
+      __syncthreads();
+      select_gate(gate_cand, count, q, c, cap, ms->shmax, gate_num, gate_den, ms);
+    }
+  } else if (P2 <= 2 * kWave) {
+    // k <= 128: one wave sorts the (at most 128) kept entries in registers,
+    // two per lane (positions lane and lane + 64), the bitonic network of the
+    // LDS sort below with shuffles instead of its 28 block barriers
+    if (tid < kWave) {
+      uint64_t a = tid < nres ? res[tid] : kEmpty;
+      uint64_t b = tid + kWave < nres ? res[tid + kWave] : kEmpty;
+      for (int size = 2; size <= 2 * kWave; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          if (stride == kWave) {  // partners in one lane; size 128: ascending
+            const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+            a = lo;
+            b = hi;
+          } else {
+            const uint64_t pa = shfl_xor_u64(a, stride), pb = shfl_xor_u64(b, stride);
+            const bool lower = (tid & stride) == 0;
+            const bool asc_a = (tid & size) == 0, asc_b = ((tid + kWave) & size) == 0;
+            a = (lower == asc_a) ? (a < pa ? a : pa) : (a < pa ? pa : a);
+            b = (lower == asc_b) ? (b < pb ? b : pb) : (b < pb ? pb : b);
+          }
+        }
+      }
+      const uint64_t e2[2] = {a, b};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = tid + h * kWave;
+        if (i < k) {
+          const uint64_t e = e2[h];
+          out_dist[q * k + i] = e == kEmpty ? __builtin_nanf("") : key_float((uint32_t)(e >> 32));
+          out_row[q * k + i] = e == kEmpty ? -1 : (int64_t)(e & 0xffffffffull);
+        }
+      }
+    }
   } else {
     for (int i = nres + tid; i < P2; i += kSelectThreads) res[i] = kEmpty;
     __syncthreads();
@@ -810,7 +892,8 @@ static int launch_select_one(const T* X, int64_t n, int d, int64_t row_base, con
                              uint32_t* count, int zero, int k, int metric, uint64_t* thr,
                              float* out_dist, int64_t* out_row, const uint64_t* alt,
                              int64_t alt_m, int64_t alt_gate, uint64_t* pre, int pre_p,
-                             hipStream_t stream) {
+                             hipStream_t stream, const uint64_t* gate_cand = nullptr,
+                             int64_t gate_num = 0, int64_t gate_den = 1) {
   const void* fn = metric == FX_METRIC_COS  ? (const void*)select_kernel<T, 2, MODE>
                    : metric == FX_METRIC_IP ? (const void*)select_kernel<T, 1, MODE>
                                             : (const void*)select_kernel<T, 0, MODE>;
@@ -832,11 +915,12 @@ static int launch_select_one(const T* X, int64_t n, int d, int64_t row_base, con
     int64_t* orow = out_row != nullptr ? out_row + q0 * k : nullptr;
     const uint64_t* aq = alt != nullptr ? alt + q0 * alt_m : nullptr;
     uint64_t* pq = pre != nullptr ? pre + q0 * (int64_t)pre_p * k : nullptr;
+    const uint64_t* gq = gate_cand != nullptr ? gate_cand + q0 * cap : nullptr;
     void* args[] = {(void*)&x,   (void*)&n,     (void*)&d,     (void*)&row_base, (void*)&qv,
                     (void*)&qnm, (void*)&kq,    (void*)&cap,   (void*)&cq,       (void*)&zero,
                     (void*)&k,   (void*)&P2,    (void*)&tq,    (void*)&od,       (void*)&orow,
                     (void*)&aq,  (void*)&alt_m, (void*)&alt_gate, (void*)&pq,    (void*)&pre_p,
-                    (void*)&pre_s};
+                    (void*)&pre_s, (void*)&gq, (void*)&gate_num, (void*)&gate_den};
     hipError_t e = hipLaunchKernel(fn, dim3(gx, (unsigned)qn), dim3(kSelectThreads), args, smem,
                                    stream);
     if (e != hipSuccess) {
@@ -855,7 +939,8 @@ static int launch_select_t(const T* X, int64_t n, int d, int64_t row_base, const
                            uint32_t* count, int zero, int k, int metric, uint64_t* thr,
                            float* out_dist, int64_t* out_row, const uint64_t* alt,
                            int64_t alt_m, int64_t alt_gate, hipStream_t stream,
-                           uint64_t* pre = nullptr) {
+                           uint64_t* pre = nullptr, const uint64_t* gate_cand = nullptr,
+                           int64_t gate_num = 0, int64_t gate_den = 1) {
   const int pre_p = pre != nullptr ? select_prune_lists(k, cap) : 0;
   if (pre_p == 0) pre = nullptr;
   if (pre != nullptr) {
@@ -866,16 +951,22 @@ static int launch_select_t(const T* X, int64_t n, int d, int64_t row_base, const
   }
   return launch_select_one<T, MODE>(X, n, d, row_base, Q, qnorm, nq, keys, cap, count, zero, k,
                                     metric, thr, out_dist, out_row, alt, alt_m, alt_gate, pre,
-                                    pre_p, stream);
+                                    pre_p, stream, gate_cand, gate_num, gate_den);
 }
 
 int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t row_base,
                            const float* Q, const float* qnorm, int64_t nq, const uint64_t* keys,
                            int64_t cap, uint32_t* count, bool zero_count, int k, int metric,
-                           uint64_t* thr, hipStream_t stream, uint64_t* prune, int64_t* topr) {
+                           uint64_t* thr, hipStream_t stream, uint64_t* prune, int64_t* topr,
+                           const uint64_t* gate_cand, int64_t gate_num, int64_t gate_den) {
   if (k > kSelectMaxK || k > cap) {
     set_error("exact threshold: k %d beyond cap %lld", k, (long long)cap);
     return FX_EUNSUPPORTED;
+  }
+  if (gate_cand != nullptr && (nq > 0x7fffffffll || gate_den <= 0 || zero_count)) {
+    set_error("exact threshold gate: nq=%lld den=%lld zero=%d", (long long)nq,
+              (long long)gate_den, (int)zero_count);
+    return FX_EINVAL;
   }
   if (prune != nullptr && topr != nullptr && select_prune_lists(k, cap) > 0) {
     // large k: the pruned select writes the k rows, the chip rescores them
@@ -890,15 +981,19 @@ int launch_exact_threshold(const void* X, int dtype, int64_t n, int d, int64_t r
                                              metric, thr, nullptr, topr, nullptr, 0, 0, stream,
                                              prune);
     if (rc) return rc;
-    return launch_exact_kth(X, dtype, n, d, row_base, Q, qnorm, nq, k, topr, metric, thr, stream);
+    rc = launch_exact_kth(X, dtype, n, d, row_base, Q, qnorm, nq, k, topr, metric, thr, stream);
+    if (rc || gate_cand == nullptr) return rc;
+    return launch_overflow_gate(gate_cand, count, thr, nq, (int)cap, gate_num, gate_den, stream);
   }
   if (dtype == FX_DTYPE_F16)
     return launch_select_t<_Float16, 0>(reinterpret_cast<const _Float16*>(X), n, d, row_base, Q,
                                         qnorm, nq, keys, cap, count, zero_count ? 1 : 0, k, metric,
-                                        thr, nullptr, nullptr, nullptr, 0, 0, stream, prune);
+                                        thr, nullptr, nullptr, nullptr, 0, 0, stream, prune,
+                                        gate_cand, gate_num, gate_den);
   return launch_select_t<float, 0>(reinterpret_cast<const float*>(X), n, d, row_base, Q, qnorm, nq,
                                    keys, cap, count, zero_count ? 1 : 0, k, metric, thr, nullptr,
-                                   nullptr, nullptr, 0, 0, stream, prune);
+                                   nullptr, nullptr, 0, 0, stream, prune, gate_cand, gate_num,
+                                   gate_den);
 }
 
 int launch_sample_threshold(const uint64_t* keys, int64_t nq, int64_t cap, uint32_t* count,

@@ -1504,6 +1504,9 @@ __device__ __forceinline__ void i8_note_row(float* rinfo, float* rterm, float* r
 
 // i3_epilogue for the int8 image: the packed pass test above (2 or 3
 // v_pk_fma_f32 and one v_pk_add_f32 per two pairs), appends with i8_bounds
+// all-pass phases of at most this many tiles reserve fixed slots even when
+// the slice shares its segments (i8_epilogue)
+constexpr int64_t kAllPassSlotTiles = 64;
 template <int METRIC>
 __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const float* rinfo,
                                             const float* rterm, const float* rext,
@@ -1558,11 +1561,13 @@ __device__ __forceinline__ void i8_epilogue(const f32x16 (&acc)[kI2QT], const fl
     pm[u] = (diag & 1) ? 0u : (~fail[u] | force) & ~smask & 0xffffu;
     if (q0 + u * 32 + l32 >= a.nq) pm[u] = 0u;
   }
-  if (a.all_pass && segcap <= FX_I3_SEG) {  // no threshold yet (first phase): every live
-                     // pair, slots reserved per lane and query, accumulators indexed
-                     // statically (a slice of few live queries appends through its
-                     // segments below instead: one query's whole sample otherwise
-                     // meets in one global counter, ~3 K atomics)
+  if (a.all_pass && (segcap <= FX_I3_SEG || a.num_tiles <= kAllPassSlotTiles)) {
+                     // no threshold yet (first phase): every live pair, slots reserved
+                     // per lane and query, accumulators indexed statically (a slice
+                     // of few live queries over a large first sample, k ~ 1 000,
+                     // appends through its segments below instead: its whole sample
+                     // otherwise meets in one global counter, ~3 K atomics; a small
+                     // one, k = 100's 20 tiles, is faster through the slots)
     static_for<kI2QT>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
       const uint32_t bits = pm[u];

@@ -948,7 +948,10 @@ def gather_rows(shards: Sequence[Shard], rows: torch.Tensor) -> Optional[torch.T
     with torch.cuda.device(dev):
         if len(shards) == 1:
             s = shards[0]
-            local = (flat - s.row_base).clamp_(0, max(s.n - 1, 0))
+            # (row_base 0, a table's first shard: one clamp launch, not a
+            # subtraction and a clamp, ~5 us of the served search's tail)
+            local = (flat.clamp(0, max(s.n - 1, 0)) if s.row_base == 0
+                     else (flat - s.row_base).clamp_(0, max(s.n - 1, 0)))
             return s.data.index_select(0, local).view(nq, kk, s.d)
         bases = torch.tensor([s.row_base for s in shards], dtype=torch.int64).to(
             dev, non_blocking=True)

@@ -68,6 +68,10 @@ for step in "$@"; do
     abseg) run abseg 1100 python -u tools/sweep.py --libs new,old --reps 2 --steps 20 --warmup 3 \
         --out gpurun_out/r06/abseg.jsonl -- "--no-batch-leg" "--no-batch-leg --nq 256 --metric cosine" \
         "$K4" ;;
+    rtrace) run rtrace 300 rocprofv3 --runtime-trace --kernel-trace --memory-copy-trace -d gpurun_out/r06/rtrace \
+        -o run --output-format csv -- python3 -u tools/profile_call.py --n 10000000 --d 768 --dtype f32 \
+        --metric l2 --k 100 --batch 1000 --reps 30
+      python tools/host_gap.py gpurun_out/r06/rtrace/run > gpurun_out/r06/rtrace_gap.txt 2>&1 ;;
     flight0) run flight0 300 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 --reps 60 ;;
     k1000) run k1000a 300 python -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
         --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024
