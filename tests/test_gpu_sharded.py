@@ -131,15 +131,19 @@ def test_configs4_50M_x1536_f16_ip_k1000_sharded_x8(eng):
     details = []
     near = check_topk(g7d.cpu().numpy(), g7r.cpu().numpy(), od, orow, sample, q, "inner_product",
                       details=details)
-    rec["shard7_vs_oracle"] = {"near_ties": near, "positions": details}
+    # (k = 1 000 takes the int8 image since round 6: record whether it served)
+    rec["shard7_vs_oracle"] = {"near_ties": near, "positions": details,
+                               "int8_image": id(shards[7].data) in eng._images}
     # and the whole 50M corpus for one query
     od, orow = O.knn_gen(N4, D4, 0, q[:1], "inner_product", K4, dtype=np.float16,
                          overrides=planted)
     details = []
-    wd, wr = eng.search([Shard(x, 0)], qt[:1], ip, K4)
+    whole = Shard(x, 0)
+    wd, wr = eng.search([whole], qt[:1], ip, K4)
     near_all = check_topk(wd.cpu().numpy(), wr.cpu().numpy(), od, orow, sample, q[:1],
                           "inner_product", details=details)
-    rec["whole_vs_oracle"] = {"near_ties": near_all, "positions": details}
+    rec["whole_vs_oracle"] = {"near_ties": near_all, "positions": details,
+                              "int8_image": id(whole.data) in eng._images}
     record("configs[4]", rec)
     print("configs[4] near-ties", near, near_all)
     assert near == 0 and near_all == 0, rec  # bit-exact ids (measured: 0 near-ties)

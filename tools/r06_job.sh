@@ -72,6 +72,16 @@ for step in "$@"; do
         -o run --output-format csv -- python3 -u tools/profile_call.py --n 10000000 --d 768 --dtype f32 \
         --metric l2 --k 100 --batch 1000 --reps 30
       python tools/host_gap.py gpurun_out/r06/rtrace/run > gpurun_out/r06/rtrace_gap.txt 2>&1 ;;
+    sq) run sq1 200 bash tools/pmc.sh img8_sq1 "GRBM_GUI_ACTIVE SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_WAVE_CYCLES" \
+        --nq 256 --metric cosine --no-verify --no-accelerated
+      run sq2 200 bash tools/pmc.sh img8_sq2 "GRBM_GUI_ACTIVE SQ_INSTS_SALU SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES" \
+        --nq 256 --metric cosine --no-verify --no-accelerated
+      python tools/sq_summary.py gpurun_out/pmc_img8_sq1/run_counter_collection.csv filter_img8 > gpurun_out/r06/sq_img8.txt
+      python tools/sq_summary.py gpurun_out/pmc_img8_sq2/run_counter_collection.csv filter_img8 >> gpurun_out/r06/sq_img8.txt ;;
+    cfg4test) run cfg4test 600 python -u -m pytest tests/test_gpu_sharded.py -m gpu -x -v -p no:cacheprovider \
+        --timeout 500 --timeout-method thread -k configs4 ;;
+    flight4) run flight4 600 python -u tools/bench_flight.py --n 6250000 --d 1536 --k 1000 --metric inner_product \
+        --dtype f16 --direct --reps 40 ;;
     flight0) run flight0 300 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 --reps 60 ;;
     k1000) run k1000a 300 python -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
         --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024
