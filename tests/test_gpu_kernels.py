@@ -1248,3 +1248,43 @@ def test_int8_large_k_pruned_selects_bit_identical(eng, metric, dtype, n, d, nq,
 
 def eng_dtype(dtype):
     return _lib.DTYPE_F16 if dtype == torch.float16 else _lib.DTYPE_F32
+
+
+@pytest.mark.parametrize("metric", METRICS)
+def test_int8_k1000_default_masked_extreme_clustered(eng, metric):
+    """k = 1 000 through the int8 image with the DEFAULT options (i8_max_k
+    1 024 since round 6; batch_min_queries = 1 only sends the single query
+    below the 4 GiB single-query rule): a mask, rows the image cannot
+    represent, a clustered corpus and a query planted inside a cluster, each
+    bit-identical to the exact scan, and the clean single query's ids
+    against the float64 oracle.  Reference: index.py:161-168 (filter, then
+    select_k_unstable with maxval 1 000)."""
+    n, d, k = 150_000, 128, 1000
+    m = _lib.METRICS[metric]
+    assert _lib.get_option("i8_max_k") >= k
+    cases = []
+    xh = _extreme_rows(n, d, 81)
+    mask = np.random.RandomState(82).rand(n) < 0.7
+    cases.append(("extreme+mask", torch.from_numpy(xh).to(eng.device), mask,
+                  O.fill_normal(1, d, seed=83)))
+    xc = gpu_fill(eng, n, d, seed=84, cluster=1000)
+    qc = O.fill_normal(n, d, 84, cluster=1000)[n // 2 : n // 2 + 1] + 0.01
+    cases.append(("clustered, query in a cluster", xc, None, qc))
+    xn = gpu_fill(eng, n, d, seed=85)
+    qn = O.fill_normal(1, d, seed=86)
+    cases.append(("clean", xn, None, qn))
+    for name, x, mk, q in cases:
+        eng.clear_images()
+        with _lib.options(batch_min_queries=1):
+            assert _lib.filter_image_used(n, d, _lib.DTYPE_F32, 1, k, m)
+            fd, fr = gpu_search(eng, x, q, metric, k, mask=mk)
+            assert id(x) in eng._images, name  # the int8 image served it
+        with _lib.options(batched=0):
+            sd, sr = gpu_search(eng, x, q, metric, k, mask=mk)
+        np.testing.assert_array_equal(fr, sr, err_msg=name)
+        np.testing.assert_array_equal(fd.view(np.uint32), sd.view(np.uint32), err_msg=name)
+        if mk is not None:
+            assert np.all(mk[fr[fr >= 0]]), name
+    od, orow = O.knn(O.fill_normal(n, d, 85), qn, metric, k)
+    check_topk(fd, fr, od, orow, O.fill_normal(n, d, 85), qn, metric)
+    eng.clear_images()

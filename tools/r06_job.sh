@@ -82,6 +82,11 @@ for step in "$@"; do
         --timeout 500 --timeout-method thread -k configs4 ;;
     flight4) run flight4 600 python -u tools/bench_flight.py --n 6250000 --d 1536 --k 1000 --metric inner_product \
         --dtype f16 --direct --reps 40 ;;
+    gsweep) run gsweep 1100 python -u tools/sweep.py --reps 2 --steps 20 --warmup 3 \
+        --out gpurun_out/r06/grow_sweep.jsonl -- "--no-batch-leg" "--no-batch-leg --opt i8_grow_ratio=32" \
+        "--no-batch-leg --opt i8_grow_ratio=64" "--no-batch-leg --opt i8_grow_ratio=128" \
+        "--no-batch-leg --opt i8_grow_ratio=64 --opt select_prune=2" \
+        "--no-batch-leg --nq 256 --metric cosine" "--no-batch-leg --nq 256 --metric cosine --opt i8_grow_ratio=64" ;;
     flight0) run flight0 300 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 --reps 60 ;;
     k1000) run k1000a 300 python -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
         --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024
