@@ -739,17 +739,23 @@ class Engine:
     def search(self, shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: int,
                masks: Optional[Sequence[Optional[torch.Tensor]]] = None,
                counts: Optional[Sequence[Optional[int]]] = None,
+               out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
                ) -> Tuple[torch.Tensor, torch.Tensor]:
         """Exact top-k over several shards (sources): per-shard scan, then merge.
-        ``counts`` (optional): rows each mask keeps, to pick the row-list scan."""
+        ``counts`` (optional): rows each mask keeps, to pick the row-list scan.
+        ``out`` (one shard only): the (dist [nq, k] f32, row [nq, k] i64)
+        tensors on this device to write into (search_host's packed result)."""
         queries = _to_device(queries, self.device)
         nq = queries.shape[0]
         mask_of = (lambda i: masks[i]) if masks else (lambda i: None)
         count_of = (lambda i: counts[i]) if counts else (lambda i: None)
+        if out is not None and len(shards) != 1:
+            raise ValueError("Engine.search: out= needs exactly one shard")
         with self.lock:
             if len(shards) == 1:
-                od = torch.empty((nq, k), dtype=torch.float32, device=self.device)
-                orow = torch.empty((nq, k), dtype=torch.int64, device=self.device)
+                od, orow = out if out is not None else (
+                    torch.empty((nq, k), dtype=torch.float32, device=self.device),
+                    torch.empty((nq, k), dtype=torch.int64, device=self.device))
                 self._search_one(shards[0], queries, metric, k, mask_of(0), count_of(0), od, orow)
                 return od, orow
             if self._one_merge(shards, nq, k, metric, masks):
@@ -995,6 +1001,44 @@ def _to_host(*ts: torch.Tensor) -> Tuple[np.ndarray, ...]:
     return tuple(h.numpy() for h in outs)
 
 
+def _search_packed(shard: Shard, queries: torch.Tensor, metric: int, k: int,
+                   masks=None, counts=None) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """One shard's search with the k winning rows gathered behind it, all
+    three results written into ONE device buffer [rows i64 | dist f32 | pad |
+    vectors] and brought back with ONE D2H and one synchronisation (three
+    copies of a served search's tail were ~15 us of it,
+    profiles/r06_flight_cfg1_host_gap.txt).  Same results as _search_all +
+    gather_rows + _to_host."""
+    dev = shard.data.device
+    nq = queries.shape[0]
+    m = nq * k
+    esz = shard.data.element_size()
+    off_d = 8 * m
+    off_v = (off_d + 4 * m + 15) // 16 * 16
+    total = off_v + m * shard.d * esz
+    with torch.cuda.device(dev):
+        packed = torch.empty(total, dtype=torch.uint8, device=dev)
+        orow = packed[:off_d].view(torch.int64).view(nq, k)
+        od = packed[off_d:off_d + 4 * m].view(torch.float32).view(nq, k)
+        vecs = packed[off_v:].view(shard.data.dtype).view(m, shard.d)
+        Engine.get(dev).search([shard], queries, metric, k, masks, counts, out=(od, orow))
+        flat = orow.reshape(-1)
+        local = (flat.clamp(0, max(shard.n - 1, 0)) if shard.row_base == 0
+                 else (flat - shard.row_base).clamp_(0, max(shard.n - 1, 0)))
+        torch.index_select(shard.data, 0, local, out=vecs)
+        host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+        host.copy_(packed, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+    hb = host.numpy()
+    return (hb[off_d:off_d + 4 * m].view(np.float32).reshape(nq, k),
+            hb[:off_d].view(np.int64).reshape(nq, k),
+            hb[off_v:].view(_np_dtype(shard.data.dtype)).reshape(nq, k, shard.d))
+
+
+def _np_dtype(dt: torch.dtype):
+    return {torch.float32: np.float32, torch.float16: np.float16, torch.uint8: np.uint8}[dt]
+
+
 def search_host(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: int,
                 masks: Optional[Sequence[Optional[torch.Tensor]]] = None,
                 counts: Optional[Sequence[Optional[int]]] = None, gather: bool = False,
@@ -1008,6 +1052,8 @@ def search_host(shards: Sequence[Shard], queries: torch.Tensor, metric: int, k: 
     devices).  A single unfiltered query goes through the serving coalescer
     like ``search_all``."""
     def run(qs: torch.Tensor, kk: int, ms=None, cs=None) -> Tuple[np.ndarray, ...]:
+        if gather and len(shards) == 1 and shards[0].n > 0:
+            return _search_packed(shards[0], qs, metric, kk, ms, cs)
         d, r = _search_all(shards, qs, metric, kk, ms, cs)
         v = gather_rows(shards, r) if gather else None
         if v is None:
