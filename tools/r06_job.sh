@@ -87,6 +87,10 @@ for step in "$@"; do
         "--no-batch-leg --opt i8_grow_ratio=64" "--no-batch-leg --opt i8_grow_ratio=128" \
         "--no-batch-leg --opt i8_grow_ratio=64 --opt select_prune=2" \
         "--no-batch-leg --nq 256 --metric cosine" "--no-batch-leg --nq 256 --metric cosine --opt i8_grow_ratio=64" ;;
+    ctrace2) run ctrace2 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r06/ctrace2 -o run \
+        --output-format csv -- python3 -u bench.py --nq 256 --metric cosine --no-cpu-baseline --steps 5 --warmup 1
+      python tools/timeline.py gpurun_out/r06/ctrace2/run_kernel_trace.csv qprep8 \
+        > gpurun_out/r06/ctrace2_timeline.txt ;;
     flight0) run flight0 300 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 --reps 60 ;;
     k1000) run k1000a 300 python -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
         --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024
