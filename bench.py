@@ -536,6 +536,7 @@ def main():
         "kernel_ms": scan_ms,
         "bytes_per_launch": scan_bytes,
         "library_sha": _lib.library_sha(),
+        "build": _lib.build_info(),
     }
     if filt:  # the GEMM the filter evaluates, against the dense MFMA peak of its type
         roof["bytes_basis"] = "filter image + row terms (the pass reads these, not the rows)"
