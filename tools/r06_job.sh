@@ -91,6 +91,12 @@ for step in "$@"; do
         --output-format csv -- python3 -u bench.py --nq 256 --metric cosine --no-cpu-baseline --steps 5 --warmup 1
       python tools/timeline.py gpurun_out/r06/ctrace2/run_kernel_trace.csv qprep8 \
         > gpurun_out/r06/ctrace2_timeline.txt ;;
+    rsweep2) C2="--no-batch-leg --nq 256 --metric cosine"
+      run rsweep2 1100 python -u tools/sweep.py --reps 2 --steps 20 --warmup 3 \
+        --out gpurun_out/r06/ratio_sweep_cfg2.jsonl -- "$C2" "$C2 --opt i8_grow_ratio=8" \
+        "$C2 --opt i8_grow_ratio=12" "$C2 --opt i8_sample_ratio=6" "$C2 --opt i8_sample_ratio=10" \
+        "$C2 --opt i8_sample_ratio=12" "--no-batch-leg --opt i8_grow_ratio=8" \
+        "--no-batch-leg --opt i8_sample_ratio=6" "--no-batch-leg --opt i8_sample_ratio=10" ;;
     flight0) run flight0 300 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 --reps 60 ;;
     k1000) run k1000a 300 python -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
         --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024
