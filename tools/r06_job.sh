@@ -97,6 +97,10 @@ for step in "$@"; do
         "$C2 --opt i8_grow_ratio=12" "$C2 --opt i8_sample_ratio=6" "$C2 --opt i8_sample_ratio=10" \
         "$C2 --opt i8_sample_ratio=12" "--no-batch-leg --opt i8_grow_ratio=8" \
         "--no-batch-leg --opt i8_sample_ratio=6" "--no-batch-leg --opt i8_sample_ratio=10" ;;
+    rsweep3) run rsweep3 1100 python -u tools/sweep.py --reps 3 --steps 30 --warmup 3 \
+        --out gpurun_out/r06/ratio_sweep_s6.jsonl -- "--no-batch-leg" "--no-batch-leg --opt i8_sample_ratio=6" \
+        "--no-batch-leg --opt i8_sample_ratio=5" "--no-batch-leg --opt i8_sample_ratio=7" \
+        "$K4" "$K4 --opt i8_sample_ratio=6" ;;
     flight0) run flight0 300 python -u tools/bench_flight.py --n 100000 --d 128 --k 10 --metric l2 --reps 60 ;;
     k1000) run k1000a 300 python -u bench.py --dtype f16 --d 1536 --rows 6250000 --k 1000 \
         --metric inner_product --no-cpu-baseline --no-batch-leg --opt i8_max_k=1024
